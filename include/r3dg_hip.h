@@ -1,0 +1,244 @@
+/*
+ * r3dg_hip.h -- C ABI of the MI355X-native relightable Gaussian-splat rasterizer.
+ *
+ * This is the drop-in boundary. Every entry point here is the plain-pointer form of one
+ * function of the reference's pybind module `r3dg_rasterization._C`
+ * (reference: r3dg-rasterization/ext.cu:21-35). The torch binding
+ * relightable3dgaussian_amd/csrc/torch_ext.cpp re-exports them under the reference's names
+ * with the reference's argument order and return tuples. No torch types appear here: device
+ * buffers are raw pointers, the stream is a hipStream_t passed as void*, and the three opaque
+ * state buffers of the reference (geomBuffer / binningBuffer / imgBuffer,
+ * rasterize_points.cu:104-111) are obtained through caller-supplied allocation callbacks, the
+ * C form of the reference's std::function<char*(size_t)> resize functors
+ * (rasterize_points.cu:31-37).
+ *
+ * Conventions (as in the reference):
+ *   - all float data is fp32, contiguous, on the current device;
+ *   - an absent optional tensor (reference: empty tensor -> nullptr) is passed as NULL;
+ *   - view/proj matrices are the transposed 4x4 torch matrices of scene/cameras.py:63-79
+ *     (element m[4*c + r] multiplies coordinate c for output r);
+ *   - image outputs are HWC (rasterize_points.cu:94-101); the feature output uses the layout
+ *     documented at r3dg_feature_groups().
+ * All functions return R3DG_OK (0) or a negative error code; r3dg_last_error() has the text.
+ */
+#ifndef R3DG_HIP_H
+#define R3DG_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define R3DG_ABI_VERSION 1
+
+enum {
+    R3DG_OK = 0,
+    R3DG_ERR_ARG = -1,         /* shape / argument error (reference: AT_ERROR -> RuntimeError) */
+    R3DG_ERR_HIP = -2,         /* HIP runtime or kernel launch failure */
+    R3DG_ERR_UNSUPPORTED = -3, /* feature outside this build's scope (DESIGN.md "Scope") */
+    R3DG_ERR_ALLOC = -4        /* an allocation callback returned NULL */
+};
+
+typedef void* r3dg_stream_t;                                 /* hipStream_t */
+typedef void* (*r3dg_alloc_fn)(void* ctx, size_t nbytes);    /* returns device memory, >= 256-B aligned */
+
+int r3dg_abi_version(void);
+const char* r3dg_last_error(void);
+
+/* Feature output layout (replaces forward.cu:537-558, DESIGN.md "Feature layout").
+ * Writes the channel-group sizes for S channels into groups[] and returns their count.
+ * A group of size n starting at channel c0 is stored as a [H*W, n] block at offset c0*H*W
+ * of the flat feature output. S=21 reproduces the reference's 3 scalar planes + six [HW,3]
+ * blocks exactly; S=11 (training) uses [1,1,3,3,3]; any other S is planar [S,H,W]. */
+int r3dg_feature_groups(int S, int* groups);
+
+/* ---- rasterizer (rasterize_points.cu:39-181, rasterizer_impl.cu:213-529) ------------------- */
+
+typedef struct r3dg_raster_settings {
+    int P;  /* number of Gaussians (means3D.size(0)) */
+    int S;  /* feature channels (features.size(1)) */
+    int D;  /* active SH degree */
+    int M;  /* SH coefficients per Gaussian (sh.size(1)), 0 if sh absent */
+    int W, H;
+    float tan_fovx, tan_fovy, cx, cy;
+    float scale_modifier;
+    float time, dt;
+    int prefiltered;
+    int compute_pseudo_normal; /* reference spelling: computer_pseudo_normal */
+    int debug;                 /* synchronise and check after every launch */
+    const float* bg;           /* [3] */
+    const float* viewmatrix;   /* [16] */
+    const float* viewmatrix_inv;
+    const float* projmatrix;
+    const float* projmatrix_inv;
+    const float* campos;       /* [3] */
+    int64_t sh_shader_manager;    /* handle from r3dg_preprocess_model, 0 = all ShDefault */
+    int64_t splat_shader_manager; /* handle from r3dg_preprocess_model, 0 = all SplatDefault */
+    int64_t texture_manager;      /* 0 = none */
+    const int64_t* post_passes;   /* host array of post-process pass handles */
+    int n_post_passes;
+} r3dg_raster_settings;
+
+typedef struct r3dg_gaussians {
+    const float* means3D;        /* [P,3] */
+    const float* features;       /* [P,S] or NULL when S == 0 */
+    const float* colors_precomp; /* [P,3] or NULL (exactly one of colors_precomp / sh) */
+    const float* opacity;        /* [P,1] */
+    const float* scales;         /* [P,3] or NULL (exactly one of scales+rotations / cov3D_precomp) */
+    const float* rotations;      /* [P,4] or NULL */
+    const float* cov3D_precomp;  /* [P,6] or NULL */
+    const float* sh;             /* [P,M,3] or NULL */
+} r3dg_gaussians;
+
+typedef struct r3dg_forward_outputs {
+    float* color;        /* [H,W,3] */
+    float* opacity;      /* [H,W,1] */
+    float* depth;        /* [H,W,1] */
+    float* stencil;      /* [H,W,1] */
+    float* feature;      /* [H,W,S] storage, layout per r3dg_feature_groups */
+    float* shader_color; /* [H,W,3] */
+    float* normal;       /* [H,W,3] pseudo normal (zero where undefined) */
+    float* surface_xyz;  /* [H,W,3] */
+    int* radii;          /* [P] */
+} r3dg_forward_outputs;
+
+/* RasterizeGaussiansCUDA (rasterize_points.cu:39-181). The image state buffer holds n_contrib
+ * (int32 [H,W]) at byte offset r3dg_image_state_n_contrib_offset(H, W). */
+int r3dg_rasterize_gaussians(const r3dg_raster_settings* settings, const r3dg_gaussians* g,
+                             const r3dg_forward_outputs* out, r3dg_alloc_fn geom_alloc, void* geom_ctx,
+                             r3dg_alloc_fn binning_alloc, void* binning_ctx, r3dg_alloc_fn image_alloc,
+                             void* image_ctx, int* num_rendered, r3dg_stream_t stream);
+
+size_t r3dg_image_state_n_contrib_offset(int H, int W);
+
+/* Debug / parity accessors into the opaque state buffers (tile keys, sort order, ranges). */
+typedef struct r3dg_binning_view {
+    const uint64_t* keys_sorted;  /* [L] tile<<32 | depth bits, ascending */
+    const uint32_t* point_list;   /* [L] Gaussian ids in sorted order (reference point_list) */
+    const uint32_t* ranges;       /* [tiles,2] from the image buffer */
+    const uint32_t* point_offsets;/* [P] inclusive scan of tiles touched */
+    const float* depths;          /* [P] */
+    const float* means2D;         /* [P,2] */
+    const float* conic_opacity;   /* [P,4] */
+    const float* rgb;             /* [P,3] */
+    const float* cov3D;           /* [P,6] */
+    const uint8_t* clamped;       /* [P] bit c = channel c clamped */
+} r3dg_binning_view;
+int r3dg_state_view(int P, int H, int W, int L, void* geom, void* binning, void* image, r3dg_binning_view* view);
+
+typedef struct r3dg_backward_grads {
+    const float* dL_dout_color;   /* colour gradient */
+    int color_hwc;                /* 0: [3,H,W] planar (reference contract, rasterize_points.cu:214-215); 1: [H,W,3] */
+    const float* dL_dout_opacity; /* [H*W] */
+    const float* dL_dout_depth;   /* [H*W] */
+    const float* dL_dout_feature; /* feature gradient */
+    int feature_native;           /* 0: [S,H,W] planar (reference, backward.cu:470-471); 1: forward output layout */
+} r3dg_backward_grads;
+
+typedef struct r3dg_backward_outputs {
+    float* dL_dmeans2D;   /* [P,3] (x, y, depth) */
+    float* dL_dcolors;    /* [P,3] */
+    float* dL_dopacity;   /* [P,1] */
+    float* dL_dmeans3D;   /* [P,3] */
+    float* dL_dfeatures;  /* [P,S] */
+    float* dL_dcov3D;     /* [P,6] */
+    float* dL_dsh;        /* [P,M,3] (may be NULL when M == 0) */
+    float* dL_dscales;    /* [P,3] */
+    float* dL_drotations; /* [P,4] */
+} r3dg_backward_outputs;
+
+/* RasterizeGaussiansBackwardCUDA (rasterize_points.cu:183-275). Every output element is written
+ * (no pre-zeroing needed). Deterministic: per-Gaussian sums have a fixed order. */
+int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* settings, const r3dg_gaussians* g,
+                                      const int* radii, const r3dg_backward_grads* grads, void* geom,
+                                      void* binning, void* image, int num_rendered, int backward_geometry,
+                                      r3dg_alloc_fn scratch_alloc, void* scratch_ctx,
+                                      const r3dg_backward_outputs* out, r3dg_stream_t stream);
+
+/* markVisible (rasterize_points.cu:277-295): present[i] = view-space z > 0.2 */
+int r3dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                      uint8_t* present, r3dg_stream_t stream);
+
+/* ---- render equation (render_equation.cu) ---------------------------------------------- */
+
+typedef struct r3dg_brdf_inputs {
+    int P, S_incident, S_direct, S_visibility, sample_num;
+    const float* base_color;     /* [P,3] */
+    const float* roughness;      /* [P,1] */
+    const float* metallic;       /* [P,1] */
+    const float* normals;        /* [P,3] */
+    const float* viewdirs;       /* [P,3] */
+    const float* incidents_shs;  /* [P,S_incident,3] */
+    const float* direct_shs;     /* [1,S_direct,3] */
+    const float* visibility_shs; /* [P,S_visibility,1] */
+} r3dg_brdf_inputs;
+
+/* RenderEquationForwardCUDA (render_equation.cu:688-726). rand_float [P,sample_num] is read
+ * only when is_training (reference draws it with torch::rand at :708). */
+int r3dg_render_equation_forward(const r3dg_brdf_inputs* in, int is_training, const float* rand_float,
+                                 float* pbr, float* incident_dirs, float* diffuse_light, r3dg_stream_t stream);
+
+/* RenderEquationForwardCUDA_complex (render_equation.cu:220-274), outputs in reference order. */
+typedef struct r3dg_brdf_complex_outputs {
+    float* pbr;                    /* [P,3] */
+    float* incident_dirs;          /* [P,Ns,3] */
+    float* incident_lights;        /* [P,Ns,3] */
+    float* local_incident_lights;  /* [P,Ns,3] */
+    float* global_incident_lights; /* [P,Ns,3] */
+    float* incident_visibility;    /* [P,Ns,1] */
+    float* diffuse_light;          /* [P,3] */
+    float* local_diffuse_light;    /* [P,3] */
+    float* accum;                  /* [P,1] */
+    float* rgb_d;                  /* [P,3] */
+    float* rgb_s;                  /* [P,3] */
+} r3dg_brdf_complex_outputs;
+int r3dg_render_equation_forward_complex(const r3dg_brdf_inputs* in, const r3dg_brdf_complex_outputs* out,
+                                         r3dg_stream_t stream);
+
+/* RenderEquationBackwardCUDA (render_equation.cu:494-547). Bug-compatible with the reference
+ * kernel except that dL_ddirect_shs is reduced deterministically (the reference races). */
+typedef struct r3dg_brdf_grads {
+    float* dL_dbase_color;     /* [P,3] */
+    float* dL_droughness;      /* [P,1] */
+    float* dL_dmetallic;       /* [P,1] */
+    float* dL_dnormals;        /* [P,3] */
+    float* dL_dviewdirs;       /* [P,3] */
+    float* dL_dincidents_shs;  /* [P,S_incident,3] */
+    float* dL_ddirect_shs;     /* [1,S_direct,3] */
+    float* dL_dvisibility_shs; /* [P,S_visibility,1] */
+} r3dg_brdf_grads;
+int r3dg_render_equation_backward(const r3dg_brdf_inputs* in, const float* incident_dirs, const float* dL_dpbr,
+                                  const float* dL_ddiffuse_light, r3dg_alloc_fn scratch_alloc, void* scratch_ctx,
+                                  const r3dg_brdf_grads* out, r3dg_stream_t stream);
+
+/* ---- shader manager (shaderManager.cu, preprocessModel.cu, ShShader.cu, splatShader.cu) ---- */
+
+enum { R3DG_SHADER_SH = 0, R3DG_SHADER_SPLAT = 1, R3DG_SHADER_POST = 2 };
+/* Name -> handle maps (GetShShaderAddressMap & co., ShShader.cu:196-230, splatShader.cu:283-333,
+ * postProcessShader.cu). Handles are opaque shader ids, not device function pointers. */
+int r3dg_shader_count(int kind);
+const char* r3dg_shader_name(int kind, int index);
+int64_t r3dg_shader_handle(int kind, int index);
+
+/* PreprocessModel (preprocessModel.cu:156-213): assigns SH and splat shaders by position
+ * (SelectShadersCUDA, :17-59) and buckets splat indices per shader. Returns two manager
+ * handles (host objects owning device index lists). */
+int r3dg_preprocess_model(int P, const float* xyz, int64_t* sh_manager, int64_t* splat_manager,
+                          r3dg_stream_t stream);
+/* Build a manager from explicit per-splat shader handles (host array [P]); the GPU-bucketing
+ * half of PreprocessModel without the position rules. */
+int r3dg_create_shader_manager(int kind, int P, const int64_t* shader_handles_host, int64_t* manager,
+                               r3dg_stream_t stream);
+int r3dg_shader_manager_info(int64_t manager, int* n_shaders, int64_t* handles, int* instance_counts);
+
+/* Texture mode helpers (utils/texture.cu EncodeTextureMode / EncodeWrapMode). */
+int r3dg_encode_texture_mode(const char* mode);
+int r3dg_encode_wrap_mode(const char* mode);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* R3DG_HIP_H */

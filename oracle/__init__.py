@@ -1,0 +1,270 @@
+"""CPU oracle -- TEST INFRASTRUCTURE ONLY (never imported by the product package).
+
+numpy/ctypes front end of r3dg_oracle.c, the C restatement of the reference hot path
+(see that file's header for per-function reference citations). Used by tests/, by
+__graft_entry__.smoke() as the checker, and by bench.py's cpu_baseline leg.
+
+Pinning: tests/test_oracle_golden.py checks this oracle against vectors produced by the
+reference's own PyTorch code (tests/golden/make_golden.py). The tile blend has no reference
+fixture; DESIGN.md "Parity" explains what pins it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(HERE, "_build", "libr3dg_oracle.so")
+_lib = None
+
+F = np.float32
+
+
+def build() -> str:
+    src = os.path.join(HERE, "r3dg_oracle.c")
+    if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return _LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(_LIB)
+        _lib.oracle_higher_msb.restype = ctypes.c_uint32
+        _lib.oracle_higher_msb.argtypes = [ctypes.c_uint32]
+    return _lib
+
+
+def _p(a):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "oracle arrays must be contiguous"
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _f(a):
+    return None if a is None else np.ascontiguousarray(a, dtype=F)
+
+
+def feature_layout(S: int, HW: int):
+    a = np.zeros(max(S, 1), np.int64)
+    m = np.zeros(max(S, 1), np.int32)
+    lib().oracle_feature_layout(ctypes.c_int(S), ctypes.c_longlong(HW), _p(a), _p(m))
+    return a[:S], m[:S]
+
+
+def planar_layout(S: int, HW: int):
+    return (np.arange(S, dtype=np.int64) * HW), np.ones(S, np.int32)
+
+
+# ---------------------------------------------------------------------------------------------
+# rasterizer
+# ---------------------------------------------------------------------------------------------
+def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales=None, rotations=None,
+                      cov3D_precomp=None, colors_precomp=None, bg=(1.0, 1.0, 1.0), scale_modifier=1.0,
+                      compute_pseudo_normal=True):
+    """Full forward of rasterize_gaussians (rasterizer_impl.cu:213-529) with default shaders.
+    Returns a dict with the reference outputs (HWC) and the binning state."""
+    L_ = lib()
+    means3D = _f(means3D)
+    P = means3D.shape[0]
+    features = _f(features) if features is not None else np.zeros((P, 0), F)
+    S = features.shape[1]
+    W, H = cam.width, cam.height
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    sh = _f(sh)
+    M = 0 if sh is None else sh.shape[1]
+    scales, rotations, cov3D_precomp, colors_precomp = map(_f, (scales, rotations, cov3D_precomp, colors_precomp))
+    opacity = _f(opacity).reshape(P)
+    view, proj, campos = _f(cam.view), _f(cam.proj), _f(cam.campos)
+    radii = np.zeros(P, np.int32)
+    means2D = np.zeros((P, 2), F)
+    depths = np.zeros(P, F)
+    cov3D = np.zeros((P, 6), F)
+    rgb = np.zeros((P, 3), F)
+    clamped = np.zeros(P, np.uint8)
+    conic = np.zeros((P, 4), F)
+    touched = np.zeros(P, np.uint32)
+    L_.oracle_preprocess(ctypes.c_int(P), ctypes.c_int(degree), ctypes.c_int(M), _p(means3D), _p(scales),
+                         ctypes.c_float(scale_modifier), _p(rotations), _p(opacity), _p(sh), _p(cov3D_precomp),
+                         _p(colors_precomp), _p(view), _p(proj), _p(campos), ctypes.c_int(W), ctypes.c_int(H),
+                         ctypes.c_float(cam.tanfovx), ctypes.c_float(cam.tanfovy), _p(radii), _p(means2D),
+                         _p(depths), _p(cov3D), _p(rgb), _p(clamped), _p(conic), _p(touched))
+    offsets = np.cumsum(touched, dtype=np.uint64).astype(np.uint32)
+    L = int(offsets[-1]) if P else 0
+    keys = np.zeros(max(L, 1), np.uint64)
+    vals = np.zeros(max(L, 1), np.uint32)
+    L_.oracle_duplicate_with_keys(ctypes.c_int(P), _p(means2D), _p(depths), _p(offsets), _p(radii), ctypes.c_int(W),
+                                  ctypes.c_int(H), _p(keys), _p(vals))
+    bit = L_.oracle_higher_msb(gx * gy)
+    keys_s = np.zeros_like(keys)
+    vals_s = np.zeros_like(vals)
+    L_.oracle_sort_pairs(ctypes.c_longlong(L), _p(keys), _p(vals), _p(keys_s), _p(vals_s), ctypes.c_int(32 + bit))
+    ranges = np.zeros((gx * gy, 2), np.uint32)
+    L_.oracle_identify_tile_ranges(ctypes.c_longlong(L), _p(keys_s), ctypes.c_int(gx * gy), _p(ranges))
+    colors = colors_precomp if colors_precomp is not None else rgb
+    bgv = np.asarray(bg, F)
+    HW = H * W
+    final_T = np.zeros(HW, F)
+    n_contrib = np.zeros(HW, np.uint32)
+    out_color = np.zeros((H, W, 3), F)
+    out_shader = np.zeros((H, W, 3), F)
+    out_opacity = np.zeros((H, W, 1), F)
+    out_depth = np.zeros((H, W, 1), F)
+    out_feature = np.zeros((H, W, S), F)
+    L_.oracle_render_forward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(S), _p(ranges), _p(vals_s),
+                             _p(means2D), _p(depths), _p(features), _p(colors), _p(colors), _p(conic), _p(bgv),
+                             _p(final_T), _p(n_contrib), _p(out_color), _p(out_opacity), _p(out_depth),
+                             _p(out_feature), _p(out_shader))
+    normal = np.zeros((H, W, 3), F)
+    xyz = np.zeros((H, W, 3), F)
+    if compute_pseudo_normal:
+        fx, fy = cam.focal
+        L_.oracle_surface_xyz_normal(ctypes.c_int(W), ctypes.c_int(H), _p(view), ctypes.c_float(fx),
+                                     ctypes.c_float(fy), ctypes.c_float(cam.cx), ctypes.c_float(cam.cy),
+                                     _p(out_opacity), _p(out_depth), _p(normal), _p(xyz))
+    return dict(num_rendered=L, color=out_color, opacity=out_opacity, depth=out_depth,
+                stencil=np.zeros((H, W, 1), F), feature=out_feature, shader_color=out_shader, normal=normal,
+                surface_xyz=xyz, radii=radii, n_contrib=n_contrib.reshape(H, W, 1), final_T=final_T,
+                keys=keys_s[:L], point_list=vals_s[:L], ranges=ranges, offsets=offsets, depths=depths,
+                means2D=means2D, conic_opacity=conic, rgb=rgb, clamped=clamped, cov3D=cov3D,
+                # inputs kept for the backward
+                _in=dict(means3D=means3D, features=features, sh=sh, degree=degree, scales=scales,
+                         rotations=rotations, cov3D_precomp=cov3D_precomp, colors_precomp=colors_precomp,
+                         scale_modifier=scale_modifier, bg=bgv, cam=cam))
+
+
+def rasterize_backward(fwd, dL_dcolor, dL_dopacity, dL_ddepth, dL_dfeature, color_hwc=False, feature_native=False,
+                       backward_geometry=True):
+    """rasterize_gaussians_backward (rasterizer_impl.cu:533-639). Grad layouts: colour CHW [3,H,W]
+    (reference) unless color_hwc; features planar [S,H,W] (reference) unless feature_native."""
+    L_ = lib()
+    i = fwd["_in"]
+    cam = i["cam"]
+    W, H = cam.width, cam.height
+    HW = H * W
+    P = i["means3D"].shape[0]
+    S = i["features"].shape[1]
+    if color_hwc:
+        ca, cm = np.arange(3, dtype=np.int64), np.full(3, 3, np.int32)
+    else:
+        ca, cm = np.arange(3, dtype=np.int64) * HW, np.ones(3, np.int32)
+    fa, fm = feature_layout(S, HW) if feature_native else planar_layout(S, HW)
+    fa = np.ascontiguousarray(fa if S else np.zeros(1, np.int64))
+    fm = np.ascontiguousarray(fm if S else np.zeros(1, np.int32))
+    colors = i["colors_precomp"] if i["colors_precomp"] is not None else fwd["rgb"]
+    dmean2D = np.zeros((P, 3), F)
+    dconic = np.zeros((P, 4), F)
+    dopac = np.zeros((P, 1), F)
+    dcol = np.zeros((P, 3), F)
+    dfeat = np.zeros((P, S), F)
+    gc, go, gd = _f(dL_dcolor), _f(dL_dopacity), _f(dL_ddepth)
+    gf = _f(dL_dfeature) if S else np.zeros(1, F)
+    L_.oracle_render_backward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(S), _p(fwd["ranges"]),
+                              _p(np.ascontiguousarray(fwd["point_list"])), _p(i["bg"]), _p(fwd["means2D"]),
+                              _p(fwd["depths"]), _p(fwd["conic_opacity"]), _p(colors), _p(i["features"]),
+                              _p(fwd["final_T"]), _p(np.ascontiguousarray(fwd["n_contrib"].reshape(-1))), _p(gc),
+                              _p(ca), _p(cm), _p(go), _p(gd), _p(gf), _p(fa), _p(fm), ctypes.c_int(int(backward_geometry)),
+                              _p(dmean2D), _p(dconic), _p(dopac), _p(dcol), _p(dfeat))
+    M = 0 if i["sh"] is None else i["sh"].shape[1]
+    dmean3D = np.zeros((P, 3), F)
+    dcov = np.zeros((P, 6), F)
+    dsh = np.zeros((P, M, 3), F)
+    dscale = np.zeros((P, 3), F)
+    drot = np.zeros((P, 4), F)
+    cov = i["cov3D_precomp"] if i["cov3D_precomp"] is not None else fwd["cov3D"]
+    L_.oracle_preprocess_backward(ctypes.c_int(P), ctypes.c_int(i["degree"]), ctypes.c_int(M), _p(i["means3D"]),
+                                  _p(fwd["radii"]), _p(i["sh"]), _p(fwd["clamped"]), _p(i["scales"]),
+                                  _p(i["rotations"]), ctypes.c_float(i["scale_modifier"]), _p(cov),
+                                  _p(_f(cam.view)), _p(_f(cam.proj)), ctypes.c_int(W), ctypes.c_int(H),
+                                  ctypes.c_float(cam.tanfovx), ctypes.c_float(cam.tanfovy), _p(_f(cam.campos)),
+                                  _p(dmean2D), _p(dconic), _p(dcol), _p(dmean3D), _p(dcov), _p(dsh), _p(dscale),
+                                  _p(drot))
+    return dict(dL_dmeans2D=dmean2D, dL_dcolors=dcol, dL_dopacity=dopac, dL_dmeans3D=dmean3D, dL_dfeatures=dfeat,
+                dL_dcov3D=dcov, dL_dsh=dsh, dL_dscales=dscale, dL_drotations=drot, dL_dconic=dconic)
+
+
+def mark_visible(means3D, view):
+    means3D = _f(means3D)
+    out = np.zeros(means3D.shape[0], np.uint8)
+    lib().oracle_mark_visible(ctypes.c_int(means3D.shape[0]), _p(means3D), _p(_f(view)), _p(out))
+    return out.astype(bool)
+
+
+def color_from_sh(means, campos, shs, degree):
+    """computeColorFromSH (forward.cu:25-76): (rgb [P,3], clamped bits [P])."""
+    means, campos, shs = _f(means), _f(campos), _f(shs)
+    P, M = shs.shape[0], shs.shape[1]
+    rgb = np.zeros((P, 3), F)
+    cl = np.zeros(P, np.uint8)
+    lib().oracle_color_from_sh_batch(ctypes.c_int(P), ctypes.c_int(degree), ctypes.c_int(M), _p(means), _p(campos),
+                                     _p(shs), _p(rgb), _p(cl))
+    return rgb, cl
+
+
+def cov3d(scales, rotations, scale_modifier=1.0):
+    """computeCov3D (forward.cu:124-158): upper triangle [P,6]."""
+    scales, rotations = _f(scales), _f(rotations)
+    out = np.zeros((scales.shape[0], 6), F)
+    lib().oracle_cov3d_batch(ctypes.c_int(scales.shape[0]), _p(scales), ctypes.c_float(scale_modifier),
+                             _p(rotations), _p(out))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# BRDF
+# ---------------------------------------------------------------------------------------------
+def _brdf_args(inp):
+    b = {k: _f(v) for k, v in inp.items()}
+    P = b["base"].shape[0]
+    return b, P, b["incidents"].shape[1], b["env"].shape[1], b["visibility"].shape[1]
+
+
+def brdf_forward(inp, sample_num=24, is_training=False, rand=None):
+    b, P, Si, Sd, Sv = _brdf_args(inp)
+    dirs = np.zeros((P, sample_num, 3), F)
+    pbr = np.zeros((P, 3), F)
+    diff = np.zeros((P, 3), F)
+    rnd = _f(rand).reshape(P, sample_num) if rand is not None else None
+    lib().oracle_render_equation_forward(ctypes.c_int(P), ctypes.c_int(Si), ctypes.c_int(Sd), ctypes.c_int(Sv),
+                                         _p(b["base"]), _p(b["rough"]), _p(b["metal"]), _p(b["normals"]),
+                                         _p(b["viewdirs"]), _p(b["incidents"]), _p(b["env"]), _p(b["visibility"]),
+                                         ctypes.c_int(sample_num), ctypes.c_int(int(is_training)), _p(rnd),
+                                         _p(dirs), _p(pbr), _p(diff))
+    return dict(pbr=pbr, incident_dirs=dirs, diffuse_light=diff)
+
+
+def brdf_forward_complex(inp, sample_num=24):
+    b, P, Si, Sd, Sv = _brdf_args(inp)
+    Ns = sample_num
+    o = dict(incident_dirs=np.zeros((P, Ns, 3), F), pbr=np.zeros((P, 3), F),
+             incident_lights=np.zeros((P, Ns, 3), F), local_incident_lights=np.zeros((P, Ns, 3), F),
+             global_incident_lights=np.zeros((P, Ns, 3), F), incident_visibility=np.zeros((P, Ns, 1), F),
+             diffuse_light=np.zeros((P, 3), F), local_diffuse_light=np.zeros((P, 3), F), accum=np.zeros((P, 1), F),
+             rgb_d=np.zeros((P, 3), F), rgb_s=np.zeros((P, 3), F))
+    lib().oracle_render_equation_forward_complex(
+        ctypes.c_int(P), ctypes.c_int(Si), ctypes.c_int(Sd), ctypes.c_int(Sv), _p(b["base"]), _p(b["rough"]),
+        _p(b["metal"]), _p(b["normals"]), _p(b["viewdirs"]), _p(b["incidents"]), _p(b["env"]), _p(b["visibility"]),
+        ctypes.c_int(Ns), _p(o["incident_dirs"]), _p(o["pbr"]), _p(o["incident_lights"]),
+        _p(o["local_incident_lights"]), _p(o["global_incident_lights"]), _p(o["incident_visibility"]),
+        _p(o["diffuse_light"]), _p(o["local_diffuse_light"]), _p(o["accum"]), _p(o["rgb_d"]), _p(o["rgb_s"]))
+    return o
+
+
+def brdf_backward(inp, incident_dirs, dL_dpbr, dL_ddiffuse, sample_num=24):
+    b, P, Si, Sd, Sv = _brdf_args(inp)
+    o = dict(base=np.zeros((P, 3), F), rough=np.zeros((P, 1), F), metal=np.zeros((P, 1), F),
+             normals=np.zeros((P, 3), F), viewdirs=np.zeros((P, 3), F), incidents=np.zeros((P, Si, 3), F),
+             env=np.zeros((1, Sd, 3), F), visibility=np.zeros((P, Sv, 1), F))
+    lib().oracle_render_equation_backward(
+        ctypes.c_int(P), ctypes.c_int(Si), ctypes.c_int(Sd), ctypes.c_int(Sv), _p(b["base"]), _p(b["rough"]),
+        _p(b["metal"]), _p(b["normals"]), _p(b["viewdirs"]), _p(b["incidents"]), _p(b["env"]), _p(b["visibility"]),
+        ctypes.c_int(sample_num), _p(_f(incident_dirs)), _p(_f(dL_dpbr)), _p(_f(dL_ddiffuse)), _p(o["base"]),
+        _p(o["rough"]), _p(o["metal"]), _p(o["normals"]), _p(o["viewdirs"]), _p(o["incidents"]), _p(o["env"]),
+        _p(o["visibility"]))
+    return o

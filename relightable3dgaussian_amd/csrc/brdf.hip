@@ -1,0 +1,525 @@
+// brdf.hip -- per-Gaussian render-equation integration (gfx950).
+//
+// Restates reference render_equation.cu: Fibonacci-hemisphere sampling rotated to the
+// normal (:89-113), SH evaluation of incident / environment / visibility light (:17-50,
+// :114-136), Lambert + SG-GGX specular (:138-161), the training forward (:552-663), the eval
+// forward with per-sample outputs (:52-187) and the backward (:277-460).
+//
+// One thread per Gaussian loops over the samples, keeping the Gaussian's SH coefficients and
+// all per-Gaussian gradient accumulators in registers; the environment SH (same for every
+// Gaussian) is read through the scalar path. The backward is bug-compatible with the
+// reference kernel (ReLU/clamp gradients never zeroed, dL_dn_d_i overwritten, no projection
+// term for the half-vector normalisation, dL_dincidents_shs bounded by S_direct) EXCEPT the
+// racy global `dL_ddirect_shs += ...` (render_equation.cu:443-445): here each block reduces its
+// Gaussians' contributions and a second kernel sums the block partials in a fixed order.
+#include "r3dg_common.h"
+#include "r3dg_kernels.h"
+
+namespace r3dg {
+
+constexpr float kPi = 3.14159f;  // the reference's literal
+
+__device__ __forceinline__ void sh_coef16(float x, float y, float z, float* coef) {
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    coef[0] = SH_C0;
+    coef[1] = -SH_C1 * y; coef[2] = SH_C1 * z; coef[3] = -SH_C1 * x;
+    coef[4] = SH_C2_0 * xy; coef[5] = SH_C2_1 * yz; coef[6] = SH_C2_2 * (2.0f * zz - xx - yy);
+    coef[7] = SH_C2_3 * xz; coef[8] = SH_C2_4 * (xx - yy);
+    coef[9] = SH_C3_0 * y * (3.0f * xx - yy); coef[10] = SH_C3_1 * xy * z;
+    coef[11] = SH_C3_2 * y * (4.0f * zz - xx - yy); coef[12] = SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+    coef[13] = SH_C3_4 * x * (4.0f * zz - xx - yy); coef[14] = SH_C3_5 * z * (xx - yy);
+    coef[15] = SH_C3_6 * x * (xx - 3.0f * yy);
+}
+
+__device__ __forceinline__ float3 fib_dir(float3 n, int ray, int Ns, float rot) {
+    const float delta = kPi * (3.0f - sqrtf(5.0f));
+    const float z = 1 - 2 * (float)ray / (2 * (float)Ns - 1);
+    const float rad = sqrtf(1 - z * z);
+    const float theta = rot + delta * ray;
+    const float y = cosf(theta) * rad, x = sinf(theta) * rad;
+    const float v1 = -n.y, v2 = n.x, v3 = 0.f;
+    const float v11 = v1 * v1, v22 = v2 * v2, v33 = v3 * v3, v12 = v1 * v2, v13 = v1 * v3, v23 = v2 * v3;
+    const float cp1 = fmaxf(n.z + 1, 0.0000001f);
+    const float ox = (1 + (-v33 - v22) / cp1) * x + (-v3 + v12 / cp1) * y + (v2 + v13 / cp1) * z;
+    const float oy = (v3 + v12 / cp1) * x + (1 + (-v33 - v11) / cp1) * y + (-v1 + v23 / cp1) * z;
+    const float oz = (-v2 + v13 / cp1) * x + (v1 + v23 / cp1) * y + (1 + (-v22 - v11) / cp1) * z;
+    const float norm = sqrtf(fmaxf(0.0000001f, ox * ox + oy * oy + oz * oz));
+    return make_float3(ox / norm, oy / norm, oz / norm);
+}
+
+struct Sample {
+    float local[3], global[3], vis, light[3];
+    float hdn, hdo, ndi, ndo, half_norm, half[3];
+    float fd[3], fs[3], D, F[3], V;
+};
+
+struct GaussBRDF {
+    float3 n, v, base;
+    float rough, metal;
+};
+
+// SH light evaluation: coefficient arrays are either register arrays (NI/ND/NV > 0, the
+// common S = 16 case) or read from memory with runtime bounds (NI = 0 generic path).
+template <int NI, int ND, int NV>
+__device__ __forceinline__ void eval_lights(const float* coef, const float* inc, int S_inc, const float* dir,
+                                            int S_dir, const float* vis, int S_vis, Sample& s) {
+    float lx = 0.f, ly = 0.f, lz = 0.f;
+    if constexpr (NI > 0) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            lx += inc[3 * i] * coef[i]; ly += inc[3 * i + 1] * coef[i]; lz += inc[3 * i + 2] * coef[i];
+        }
+    } else {
+        for (int i = 0; i < S_inc; ++i) {
+            lx += inc[3 * i] * coef[i]; ly += inc[3 * i + 1] * coef[i]; lz += inc[3 * i + 2] * coef[i];
+        }
+    }
+    s.local[0] = fmaxf(lx, 0.0f); s.local[1] = fmaxf(ly, 0.0f); s.local[2] = fmaxf(lz, 0.0f);
+    float gx = 0.5f, gy = 0.5f, gz = 0.5f;
+    if constexpr (ND > 0) {
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+            gx += dir[3 * i] * coef[i]; gy += dir[3 * i + 1] * coef[i]; gz += dir[3 * i + 2] * coef[i];
+        }
+    } else {
+        for (int i = 0; i < S_dir; ++i) {
+            gx += dir[3 * i] * coef[i]; gy += dir[3 * i + 1] * coef[i]; gz += dir[3 * i + 2] * coef[i];
+        }
+    }
+    s.global[0] = fmaxf(gx, 0.0f); s.global[1] = fmaxf(gy, 0.0f); s.global[2] = fmaxf(gz, 0.0f);
+    float vv = 0.5f;
+    if constexpr (NV > 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) vv += vis[i] * coef[i];
+    } else {
+        for (int i = 0; i < S_vis; ++i) vv += vis[i] * coef[i];
+    }
+    s.vis = fmaxf(0.0f, fminf(vv, 1.0f));
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s.light[c] = s.vis * s.global[c] + s.local[c];
+}
+
+__device__ __forceinline__ void eval_brdf(const GaussBRDF& G, float3 d, Sample& s) {
+    const float hx = d.x + G.v.x, hy = d.y + G.v.y, hz = d.z + G.v.z;
+    s.half_norm = fmaxf(sqrtf(hx * hx + hy * hy + hz * hz), 0.0000001f);
+    s.half[0] = hx / s.half_norm; s.half[1] = hy / s.half_norm; s.half[2] = hz / s.half_norm;
+    s.hdn = fmaxf(s.half[0] * G.n.x + s.half[1] * G.n.y + s.half[2] * G.n.z, 0.0f);
+    s.hdo = fmaxf(s.half[0] * G.v.x + s.half[1] * G.v.y + s.half[2] * G.v.z, 0.0f);
+    s.ndi = fmaxf(G.n.x * d.x + G.n.y * d.y + G.n.z * d.z, 0.0f);
+    s.ndo = fmaxf(G.n.x * G.v.x + G.n.y * G.v.y + G.n.z * G.v.z, 0.0f);
+    const float base[3] = {G.base.x, G.base.y, G.base.z};
+    const float r2 = fmaxf(G.rough * G.rough, 0.0000001f);
+    const float amp = 1.0f / (r2 * kPi), sharp = 2.0f / r2;
+    s.D = amp * expf(sharp * (s.hdn - 1.0f));
+    const float p5 = powf(1.0f - s.hdo, 5.0f);
+    const float r2v = powf(1.0f + G.rough, 2.0f) / 8.0f;
+    s.V = (0.5f / fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f)) * (0.5f / fmaxf(s.ndo * (1 - r2v) + r2v, 0.0000001f));
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        s.fd[c] = (1 - G.metal) * base[c] / kPi;
+        const float F0 = 0.04f * (1.0f - G.metal) + base[c] * G.metal;
+        s.F[c] = F0 + (1.0f - F0) * p5;
+        s.fs[c] = s.D * s.F[c] * s.V;
+    }
+}
+
+struct BrdfKArgs {
+    r3dg_brdf_inputs in;
+    int is_training;
+    const float* rand_float;
+    // training forward outputs
+    float* pbr;
+    float* incident_dirs;
+    float* diffuse;
+    // complex outputs
+    r3dg_brdf_complex_outputs cx;
+    // backward
+    const float* dirs_in;
+    const float* dL_dpbr;
+    const float* dL_ddiff;
+    r3dg_brdf_grads gr;
+    float* dir_partials;  // [gridDim.x, S_direct*3]
+};
+
+template <int NI, int ND, int NV>
+__device__ __forceinline__ void load_gauss(const r3dg_brdf_inputs& in, int idx, GaussBRDF& G, float* inc, float* vis) {
+    G.n = make_float3(in.normals[3 * idx], in.normals[3 * idx + 1], in.normals[3 * idx + 2]);
+    G.v = make_float3(in.viewdirs[3 * idx], in.viewdirs[3 * idx + 1], in.viewdirs[3 * idx + 2]);
+    G.base = make_float3(in.base_color[3 * idx], in.base_color[3 * idx + 1], in.base_color[3 * idx + 2]);
+    G.rough = in.roughness[idx];
+    G.metal = in.metallic[idx];
+    if constexpr (NI > 0) {
+#pragma unroll
+        for (int i = 0; i < 3 * NI; ++i) inc[i] = in.incidents_shs[(size_t)idx * 3 * NI + i];
+    }
+    if constexpr (NV > 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) vis[i] = in.visibility_shs[(size_t)idx * NV + i];
+    }
+}
+
+// render_equation.cu:552-663 (training forward) and :52-187 (complex) share this kernel.
+template <int NI, int ND, int NV, bool COMPLEX>
+__global__ void __launch_bounds__(256) brdf_fwd_kernel(BrdfKArgs a) {
+    const r3dg_brdf_inputs& in = a.in;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= in.P) return;
+    GaussBRDF G;
+    float inc_r[NI > 0 ? 3 * NI : 1], vis_r[NV > 0 ? NV : 1];
+    load_gauss<NI, ND, NV>(in, idx, G, inc_r, vis_r);
+    const float* inc_g = in.incidents_shs + (size_t)idx * 3 * in.S_incident;
+    const float* vis_g = in.visibility_shs + (size_t)idx * in.S_visibility;
+    const int Ns = in.sample_num;
+    float pbr[3] = {0.f, 0.f, 0.f}, dl[3] = {0.f, 0.f, 0.f}, ldl[3] = {0.f, 0.f, 0.f};
+    float rd[3] = {0.f, 0.f, 0.f}, rs[3] = {0.f, 0.f, 0.f};
+    for (int r = 0; r < Ns; ++r) {
+        const size_t w = (size_t)idx * Ns + r;
+        float rot = 0.f;
+        if (!COMPLEX && a.is_training) rot = a.rand_float[w] * 2 * kPi;
+        const float3 d = fib_dir(G.n, r, Ns, rot);
+        float coef[16];
+        sh_coef16(d.x, d.y, d.z, coef);
+        Sample s;
+        if constexpr (NI > 0)
+            eval_lights<NI, ND, NV>(coef, inc_r, NI, in.direct_shs, ND, vis_r, NV, s);
+        else
+            eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, in.direct_shs, in.S_direct, vis_g, in.S_visibility, s);
+        eval_brdf(G, d, s);
+        const float tmp = 2.0f * kPi * s.ndi / (float)Ns;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float tr = s.light[c] * tmp;
+            if constexpr (COMPLEX) {
+                dl[c] += tr;
+                ldl[c] += s.local[c] * tmp;
+                rd[c] += s.fd[c] * tr;
+                rs[c] += s.fs[c] * tr;
+            } else {
+                pbr[c] += (s.fd[c] + s.fs[c]) * tr;
+                dl[c] += tr;
+            }
+        }
+        if constexpr (COMPLEX) {
+            const r3dg_brdf_complex_outputs& o = a.cx;
+            o.incident_dirs[3 * w] = d.x; o.incident_dirs[3 * w + 1] = d.y; o.incident_dirs[3 * w + 2] = d.z;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                o.incident_lights[3 * w + c] = s.light[c];
+                o.local_incident_lights[3 * w + c] = s.local[c];
+                o.global_incident_lights[3 * w + c] = s.vis * s.global[c];
+            }
+            o.incident_visibility[w] = s.vis;
+        } else {
+            a.incident_dirs[3 * w] = d.x; a.incident_dirs[3 * w + 1] = d.y; a.incident_dirs[3 * w + 2] = d.z;
+        }
+    }
+    if constexpr (COMPLEX) {
+        const r3dg_brdf_complex_outputs& o = a.cx;
+        float av[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) av[c] = dl[c] / kPi + rs[c];
+        o.accum[idx] = (av[0] + av[1] + av[2]) / 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            o.pbr[3 * idx + c] = rd[c] + rs[c];
+            o.rgb_d[3 * idx + c] = rd[c];
+            o.rgb_s[3 * idx + c] = rs[c];
+            o.diffuse_light[3 * idx + c] = dl[c];
+            o.local_diffuse_light[3 * idx + c] = ldl[c];
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            a.pbr[3 * idx + c] = pbr[c];
+            a.diffuse[3 * idx + c] = dl[c];
+        }
+    }
+}
+
+// render_equation.cu:277-460 (bug-compatible, see header). ND must be > 0 here (register
+// accumulators for the environment-SH gradient); S_direct <= 16 is checked on the host.
+template <int NI, int ND, int NV>
+__global__ void __launch_bounds__(256) brdf_bwd_kernel(BrdfKArgs a) {
+    constexpr int NDA = 16;  // register accumulators for dL_ddirect_shs (S_direct <= 16)
+    const r3dg_brdf_inputs& in = a.in;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = idx < in.P;
+    const int S_dir = in.S_direct;
+    float ddir[3 * NDA];
+#pragma unroll
+    for (int i = 0; i < 3 * NDA; ++i) ddir[i] = 0.f;
+    if (valid) {
+        GaussBRDF G;
+        float inc_r[NI > 0 ? 3 * NI : 1], vis_r[NV > 0 ? NV : 1];
+        load_gauss<NI, ND, NV>(in, idx, G, inc_r, vis_r);
+        const float* inc_g = in.incidents_shs + (size_t)idx * 3 * in.S_incident;
+        const float* vis_g = in.visibility_shs + (size_t)idx * in.S_visibility;
+        const int Ns = in.sample_num;
+        const float K = 2.0f * kPi / (float)Ns;
+        const float gp[3] = {a.dL_dpbr[3 * idx], a.dL_dpbr[3 * idx + 1], a.dL_dpbr[3 * idx + 2]};
+        const float gdl[3] = {a.dL_ddiff[3 * idx], a.dL_ddiff[3 * idx + 1], a.dL_ddiff[3 * idx + 2]};
+        const float n[3] = {G.n.x, G.n.y, G.n.z}, v[3] = {G.v.x, G.v.y, G.v.z};
+        const float b[3] = {G.base.x, G.base.y, G.base.z};
+        float dinc_r[NI > 0 ? 3 * NI : 1], dvis_r[NV > 0 ? NV : 1];
+#pragma unroll
+        for (int i = 0; i < (NI > 0 ? 3 * NI : 1); ++i) dinc_r[i] = 0.f;
+#pragma unroll
+        for (int i = 0; i < (NV > 0 ? NV : 1); ++i) dvis_r[i] = 0.f;
+        float* dinc_g = a.gr.dL_dincidents_shs + (size_t)idx * 3 * in.S_incident;
+        float* dvis_g = a.gr.dL_dvisibility_shs + (size_t)idx * in.S_visibility;
+        if (NI == 0) for (int i = 0; i < 3 * in.S_incident; ++i) dinc_g[i] = 0.f;
+        if (NV == 0) for (int i = 0; i < in.S_visibility; ++i) dvis_g[i] = 0.f;
+        float dbase_acc[3] = {0.f, 0.f, 0.f}, dn_acc[3] = {0.f, 0.f, 0.f}, dv_acc[3] = {0.f, 0.f, 0.f};
+        float dmetal_acc = 0.f, drough_acc = 0.f;
+        const int n_inc_upd = min(S_dir, in.S_incident);  // reference loop bound is S_direct (:450)
+        for (int r = 0; r < Ns; ++r) {
+            const size_t w = (size_t)idx * Ns + r;
+            const float3 d = make_float3(a.dirs_in[3 * w], a.dirs_in[3 * w + 1], a.dirs_in[3 * w + 2]);
+            const float dd[3] = {d.x, d.y, d.z};
+            float coef[16];
+            sh_coef16(d.x, d.y, d.z, coef);
+            Sample s;
+            if constexpr (NI > 0)
+                eval_lights<NI, ND, NV>(coef, inc_r, NI, in.direct_shs, ND, vis_r, NV, s);
+            else
+                eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, in.direct_shs, S_dir, vis_g, in.S_visibility, s);
+            eval_brdf(G, d, s);
+            const float rough = G.rough, metal = G.metal;
+            const float r2 = fmaxf(rough * rough, 0.0000001f);
+            const float amp = 1.0f / (r2 * kPi), sharp = 2.0f / r2;
+            const float e_amp = expf(sharp * (s.hdn - 1.0f));
+            const float r2v = powf(1.0f + rough, 2.0f) / 8.0f;
+            const float den1 = fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f);
+            const float den2 = fmaxf(s.ndo * (1 - r2v) + r2v, 0.0000001f);
+            const float g1 = 0.5f / den1, g2 = 0.5f / den2;
+            const float Tn = 2.0f * kPi * s.ndi / (float)Ns;
+            float dfd[3], dfs[3], dli[3], fsum[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                fsum[c] = s.fd[c] + s.fs[c];
+                dfd[c] = gp[c] * s.light[c] * Tn;
+                dfs[c] = gp[c] * s.light[c] * Tn;
+                dli[c] = gp[c] * fsum[c] * Tn;
+            }
+            float dndi = (gp[0] * (fsum[0] * s.light[0]) + gp[1] * (fsum[1] * s.light[1]) +
+                          gp[2] * (fsum[2] * s.light[2])) * K;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dli[c] += gdl[c] * Tn;
+            dndi += gdl[0] * (s.light[0] * K) + gdl[1] * (s.light[1] * K) + gdl[2] * (s.light[2] * K);
+            (void)dndi;  // overwritten below, as in the reference (:403)
+            float dbase[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dbase[c] = dfd[c] * (1 - metal) / kPi;
+            float dmetal = -(dfd[0] * b[0] + dfd[1] * b[1] + dfd[2] * b[2]) / kPi;
+            const float dD = dfs[0] * s.V * s.F[0] + dfs[1] * s.V * s.F[1] + dfs[2] * s.V * s.F[2];
+            float dF[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dF[c] = dfs[c] * s.D * s.V;
+            const float dV = dfs[0] * s.D * s.F[0] + dfs[1] * s.D * s.F[1] + dfs[2] * s.D * s.F[2];
+            const float damp = dD * e_amp, de = dD * amp;
+            const float dsharp = (s.hdn - 1.0f) * e_amp * de;
+            const float dhdn = sharp * e_amp * de;
+            const float dr2 = -2.0f / (r2 * r2) * dsharp - 1.0f / (r2 * r2 * kPi) * damp;
+            float drough = dr2 * 2.0f * rough;
+            const float p5 = powf(1.0f - s.hdo, 5.0f), p4 = powf(1.0f - s.hdo, 4.0f);
+            float dF0[3], dhdo = 0.f;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float F0 = 0.04f * (1.0f - metal) + b[c] * metal;
+                dF0[c] = (1.0f - p5) * dF[c];
+                dhdo += (1.0f - F0) * dF[c];
+            }
+            dhdo = dhdo * -5.0f * p4;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dbase[c] += metal * dF0[c];
+            dmetal += (b[0] - 0.04f) * dF0[0] + (b[1] - 0.04f) * dF0[1] + (b[2] - 0.04f) * dF0[2];
+            const float dg1 = dV * g2, dg2 = dV * g1;
+            const float dden1 = -0.5f / (den1 * den1) * dg1, dden2 = -0.5f / (den2 * den2) * dg2;
+            const float dndi2 = dden1 * (1 - r2v);
+            const float dndo = dden2 * (1 - r2v);
+            const float dr2v = (1.0f - s.ndi) * dden1 + (1.0f - s.ndo) * dden2;
+            drough += (1.0f + rough) / 4.0f * dr2v;
+            float dhalf[3] = {0.f, 0.f, 0.f}, dn[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f};
+            if (s.hdn > 0.0f) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { dhalf[c] += n[c] * dhdn; dn[c] += s.half[c] * dhdn; }
+            }
+            if (s.hdo > 0.0f) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { dhalf[c] += v[c] * dhdo; dv[c] += s.half[c] * dhdo; }
+            }
+            if (s.ndi > 0.0f) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) dn[c] += dd[c] * dndi2;
+            }
+            if (s.ndo > 0.0f) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { dn[c] += v[c] * dndo; dv[c] += n[c] * dndo; }
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] / s.half_norm;
+            float dglob[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dglob[c] = dli[c] * s.vis;
+            const float dvis_s = dli[0] * s.global[0] + dli[1] * s.global[1] + dli[2] * s.global[2];
+            if constexpr (NV > 0) {
+#pragma unroll
+                for (int i = 0; i < NV; ++i) dvis_r[i] += dvis_s * coef[i];
+            } else {
+                for (int i = 0; i < in.S_visibility; ++i) dvis_g[i] += dvis_s * coef[i];
+            }
+#pragma unroll
+            for (int i = 0; i < NDA; ++i)
+                if (i < S_dir) {
+                    ddir[3 * i] += dglob[0] * coef[i];
+                    ddir[3 * i + 1] += dglob[1] * coef[i];
+                    ddir[3 * i + 2] += dglob[2] * coef[i];
+                }
+            if constexpr (NI > 0) {
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+                    if (i < n_inc_upd) {
+                        dinc_r[3 * i] += dli[0] * coef[i];
+                        dinc_r[3 * i + 1] += dli[1] * coef[i];
+                        dinc_r[3 * i + 2] += dli[2] * coef[i];
+                    }
+            } else {
+                for (int i = 0; i < n_inc_upd; ++i)
+                    for (int c = 0; c < 3; ++c) dinc_g[3 * i + c] += dli[c] * coef[i];
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                dv_acc[c] += dv[c];
+                dn_acc[c] += dn[c];
+                dbase_acc[c] += dbase[c];
+            }
+            dmetal_acc += dmetal;
+            drough_acc += drough;
+        }
+        if constexpr (NI > 0) {
+#pragma unroll
+            for (int i = 0; i < 3 * NI; ++i) dinc_g[i] = dinc_r[i];
+        }
+        if constexpr (NV > 0) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) dvis_g[i] = dvis_r[i];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            a.gr.dL_dbase_color[3 * idx + c] = dbase_acc[c];
+            a.gr.dL_dnormals[3 * idx + c] = dn_acc[c];
+            a.gr.dL_dviewdirs[3 * idx + c] = dv_acc[c];
+        }
+        a.gr.dL_dmetallic[idx] = dmetal_acc;
+        a.gr.dL_droughness[idx] = drough_acc;
+    }
+    // deterministic block partial of dL_ddirect_shs
+    __shared__ float s_part[4][3 * NDA];
+    const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 3 * NDA; ++i) {
+        const float sum = wave_sum_to_lane63(ddir[i]);
+        if (l == 63) s_part[wv][i] = sum;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * NDA) {
+        const int i = threadIdx.x;
+        a.dir_partials[(size_t)blockIdx.x * 3 * NDA + i] = ((s_part[0][i] + s_part[1][i]) + s_part[2][i]) + s_part[3][i];
+    }
+}
+
+__global__ void __launch_bounds__(64) brdf_dir_reduce_kernel(const float* partials, int nblocks, int n, float* out) {
+    const int i = threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int b = 0; b < nblocks; ++b) s += partials[(size_t)b * 48 + i];
+    out[i] = s;
+}
+
+template <bool COMPLEX>
+static hipError_t launch_fwd(const BrdfKArgs& a, hipStream_t st) {
+    const r3dg_brdf_inputs& in = a.in;
+    const dim3 grid((in.P + 255) / 256), block(256);
+    if (in.S_incident == 16 && in.S_direct == 16 && in.S_visibility == 16)
+        hipLaunchKernelGGL((brdf_fwd_kernel<16, 16, 16, COMPLEX>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((brdf_fwd_kernel<0, 0, 0, COMPLEX>), grid, block, 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace r3dg
+
+using namespace r3dg;
+
+static int check_brdf_inputs(const r3dg_brdf_inputs* in) {
+    R3DG_REQUIRE(in && in->P >= 0 && in->sample_num >= 0, "render_equation: invalid sizes");
+    R3DG_REQUIRE(in->S_incident <= 16 && in->S_direct <= 16 && in->S_visibility <= 16,
+                 "render_equation: at most 16 SH coefficients (degree 3) are supported, as the reference "
+                 "computeSHcoef(3) (render_equation.cu:17-50)");
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_render_equation_forward(const r3dg_brdf_inputs* in, int is_training, const float* rand_float,
+                                            float* pbr, float* incident_dirs, float* diffuse_light,
+                                            r3dg_stream_t stream) {
+    int rc = check_brdf_inputs(in);
+    if (rc) return rc;
+    R3DG_REQUIRE(!is_training || rand_float || in->P == 0, "render_equation_forward: training needs rand_float");
+    if (in->P == 0) return R3DG_OK;
+    BrdfKArgs a{};
+    a.in = *in;
+    a.is_training = is_training;
+    a.rand_float = rand_float;
+    a.pbr = pbr;
+    a.incident_dirs = incident_dirs;
+    a.diffuse = diffuse_light;
+    R3DG_CHECK_HIP(launch_fwd<false>(a, (hipStream_t)stream));
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_render_equation_forward_complex(const r3dg_brdf_inputs* in, const r3dg_brdf_complex_outputs* out,
+                                                    r3dg_stream_t stream) {
+    int rc = check_brdf_inputs(in);
+    if (rc) return rc;
+    if (in->P == 0) return R3DG_OK;
+    BrdfKArgs a{};
+    a.in = *in;
+    a.cx = *out;
+    R3DG_CHECK_HIP(launch_fwd<true>(a, (hipStream_t)stream));
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_render_equation_backward(const r3dg_brdf_inputs* in, const float* incident_dirs,
+                                             const float* dL_dpbr, const float* dL_ddiffuse_light,
+                                             r3dg_alloc_fn scratch_alloc, void* scratch_ctx, const r3dg_brdf_grads* out,
+                                             r3dg_stream_t stream) {
+    int rc = check_brdf_inputs(in);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = (in->P + 255) / 256;
+    if (in->P == 0) {
+        R3DG_CHECK_HIP(hipMemsetAsync(out->dL_ddirect_shs, 0, sizeof(float) * 3 * in->S_direct, st));
+        return R3DG_OK;
+    }
+    float* partials = (float*)scratch_alloc(scratch_ctx, sizeof(float) * 48 * (size_t)nb);
+    if (!partials) {
+        set_error("render_equation_backward: scratch allocation failed");
+        return R3DG_ERR_ALLOC;
+    }
+    BrdfKArgs a{};
+    a.in = *in;
+    a.dirs_in = incident_dirs;
+    a.dL_dpbr = dL_dpbr;
+    a.dL_ddiff = dL_ddiffuse_light;
+    a.gr = *out;
+    a.dir_partials = partials;
+    if (in->S_incident == 16 && in->S_direct == 16 && in->S_visibility == 16)
+        hipLaunchKernelGGL((brdf_bwd_kernel<16, 16, 16>), dim3(nb), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((brdf_bwd_kernel<0, 0, 0>), dim3(nb), dim3(256), 0, st, a);
+    R3DG_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(brdf_dir_reduce_kernel, dim3(1), dim3(64), 0, st, partials, nb, 3 * in->S_direct,
+                       out->dL_ddirect_shs);
+    R3DG_CHECK_HIP(hipGetLastError());
+    return R3DG_OK;
+}

@@ -1,0 +1,202 @@
+// preprocess.hip -- per-Gaussian projection, tile binning keys and tile ranges (gfx950).
+//
+// Restates reference forward.cu:25-267 (preprocessCUDA, computeColorFromSH, computeCov3D,
+// computeCov2D), rasterizer_impl.cu:56-140 (checkFrustum, duplicateWithKeys,
+// identifyTileRanges). Everything that feeds the tile|depth keys is evaluated as plain IEEE
+// ops in a fixed order with FP contraction OFF, matching oracle/r3dg_oracle.c bit for bit, so
+// the keys and the sort order are reproducible (SURVEY.md §7 "Bit-exact keys").
+#pragma clang fp contract(off)
+
+#include "r3dg_common.h"
+#include "r3dg_kernels.h"
+
+namespace r3dg {
+
+// forward.cu:25-76.  Writes rgb and the clamp bits.
+__device__ static void color_from_sh(int deg, float3 pos, const float* campos, const float* sh, float* rgb,
+                                     uint8_t* clamped) {
+    float dx = pos.x - campos[0], dy = pos.y - campos[1], dz = pos.z - campos[2];
+    float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    float x = dx / len, y = dy / len, z = dz / len;
+    float xx = x * x, yy = y * y, zz = z * z;
+    float xy = x * y, yz = y * z, xz = x * z;
+    uint8_t cl = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float r = SH_C0 * sh[0 * 3 + c];
+        if (deg > 0) {
+            r = r - SH_C1 * y * sh[1 * 3 + c] + SH_C1 * z * sh[2 * 3 + c] - SH_C1 * x * sh[3 * 3 + c];
+            if (deg > 1) {
+                r = r + SH_C2_0 * xy * sh[4 * 3 + c] + SH_C2_1 * yz * sh[5 * 3 + c] +
+                    SH_C2_2 * (2.0f * zz - xx - yy) * sh[6 * 3 + c] + SH_C2_3 * xz * sh[7 * 3 + c] +
+                    SH_C2_4 * (xx - yy) * sh[8 * 3 + c];
+                if (deg > 2) {
+                    r = r + SH_C3_0 * y * (3.0f * xx - yy) * sh[9 * 3 + c] + SH_C3_1 * xy * z * sh[10 * 3 + c] +
+                        SH_C3_2 * y * (4.0f * zz - xx - yy) * sh[11 * 3 + c] +
+                        SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * sh[12 * 3 + c] +
+                        SH_C3_4 * x * (4.0f * zz - xx - yy) * sh[13 * 3 + c] +
+                        SH_C3_5 * z * (xx - yy) * sh[14 * 3 + c] + SH_C3_6 * x * (xx - 3.0f * yy) * sh[15 * 3 + c];
+                }
+            }
+        }
+        r += 0.5f;
+        if (r < 0) cl |= (uint8_t)(1u << c);
+        rgb[c] = r < 0.0f ? 0.0f : r;
+    }
+    *clamped = cl;
+}
+
+// forward.cu:124-158 (quaternion not normalised; R is the glm column-major matrix read as rows)
+__device__ static void compute_cov3d(float3 s_in, float mod, float4 q, float* cov3D) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    float R[3][3];
+    R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y + r * z); R[0][2] = 2.f * (x * z - r * y);
+    R[1][0] = 2.f * (x * y - r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z + r * x);
+    R[2][0] = 2.f * (x * z + r * y); R[2][1] = 2.f * (y * z - r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+    const float s[3] = {mod * s_in.x, mod * s_in.y, mod * s_in.z};
+    float M[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) M[i][j] = s[i] * R[i][j];
+    cov3D[0] = M[0][0] * M[0][0] + M[1][0] * M[1][0] + M[2][0] * M[2][0];
+    cov3D[1] = M[0][0] * M[0][1] + M[1][0] * M[1][1] + M[2][0] * M[2][1];
+    cov3D[2] = M[0][0] * M[0][2] + M[1][0] * M[1][2] + M[2][0] * M[2][2];
+    cov3D[3] = M[0][1] * M[0][1] + M[1][1] * M[1][1] + M[2][1] * M[2][1];
+    cov3D[4] = M[0][1] * M[0][2] + M[1][1] * M[1][2] + M[2][1] * M[2][2];
+    cov3D[5] = M[0][2] * M[0][2] + M[1][2] * M[1][2] + M[2][2] * M[2][2];
+}
+
+// forward.cu:79-118: returns (a, b, c) of the low-pass-filtered 2D covariance.
+__device__ static float3 compute_cov2d(float3 mean, float fx, float fy, float tanx, float tany, const float* cov3D,
+                                       const float* view) {
+    float3 t = xform_point4x3(mean, view);
+    const float limx = 1.3f * tanx, limy = 1.3f * tany;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float j00 = fx / t.z, j11 = fy / t.z;
+    const float j20 = -(fx * t.x) / (t.z * t.z);
+    const float j21 = -(fy * t.y) / (t.z * t.z);
+    float g0[3], g1[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        g0[r] = view[4 * r + 0] * j00 + view[4 * r + 2] * j20;
+        g1[r] = view[4 * r + 1] * j11 + view[4 * r + 2] * j21;
+    }
+    const float* c = cov3D;
+    float u0 = c[0] * g0[0] + c[1] * g0[1] + c[2] * g0[2];
+    float u1 = c[1] * g0[0] + c[3] * g0[1] + c[4] * g0[2];
+    float u2 = c[2] * g0[0] + c[4] * g0[1] + c[5] * g0[2];
+    float v0 = c[0] * g1[0] + c[1] * g1[1] + c[2] * g1[2];
+    float v1 = c[1] * g1[0] + c[3] * g1[1] + c[4] * g1[2];
+    float v2 = c[2] * g1[0] + c[4] * g1[1] + c[5] * g1[2];
+    return make_float3(g0[0] * u0 + g0[1] * u1 + g0[2] * u2 + 0.3f, g1[0] * u0 + g1[1] * u1 + g1[2] * u2,
+                       g1[0] * v0 + g1[1] * v1 + g1[2] * v2 + 0.3f);
+}
+
+// forward.cu:161-267 (preprocessCUDA)
+__global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    a.radii[idx] = 0;
+    a.tiles_touched[idx] = 0;
+    const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    const float3 pv = xform_point4x3(p, a.view);
+    if (pv.z <= 0.2f) {  // auxiliary.h:154 (the reference __trap()s when prefiltered; we flag it)
+        if (a.prefiltered && a.error_flag) atomicOr(a.error_flag, 1u);
+        return;
+    }
+    const float4 ph = xform_point4x4(p, a.proj);
+    const float p_w = 1.0f / (ph.w + 0.0000001f);
+    const float ppx = ph.x * p_w, ppy = ph.y * p_w;
+    const float* cov3D;
+    if (a.cov3D_precomp) {
+        cov3D = a.cov3D_precomp + 6 * idx;
+    } else {
+        const float3 s = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+        const float4 q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2],
+                                     a.rotations[4 * idx + 3]);
+        compute_cov3d(s, a.scale_modifier, q, a.cov3D + 6 * idx);
+        cov3D = a.cov3D + 6 * idx;
+    }
+    const float3 cov = compute_cov2d(p, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, cov3D, a.view);
+    const float det = cov.x * cov.z - cov.y * cov.y;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
+    const float mid = 0.5f * (cov.x + cov.z);
+    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+    const float px = ndc2pix(ppx, a.W), py = ndc2pix(ppy, a.H);
+    int x0, y0, x1, y1;
+    get_rect(px, py, (int)my_radius, a.grid_x, a.grid_y, x0, y0, x1, y1);
+    if ((x1 - x0) * (y1 - y0) == 0) return;
+    if (!a.colors_precomp)
+        color_from_sh(a.D, p, a.campos, a.sh + (size_t)idx * a.M * 3, a.rgb + 3 * idx, a.clamped + idx);
+    a.depths[idx] = pv.z;
+    a.radii[idx] = (int)my_radius;
+    a.means2D[idx] = make_float2(px, py);
+    a.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, a.opacity[idx]);
+    a.tiles_touched[idx] = (uint32_t)((y1 - y0) * (x1 - x0));
+}
+
+// rasterizer_impl.cu:56-68 (checkFrustum)
+__global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* __restrict__ means3D,
+                                                           const float* __restrict__ view, uint8_t* present) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const float3 p = make_float3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
+    present[idx] = xform_point4x3(p, view).z <= 0.2f ? 0 : 1;
+}
+
+// rasterizer_impl.cu:72-113 (duplicateWithKeys). The value sorted alongside each key is its
+// unsorted slot, so the sort permutation can route backward contributions to Gaussian-
+// contiguous rows; gid_of_slot maps a slot back to its Gaussian.
+__global__ void __launch_bounds__(256) duplicate_keys_kernel(int P, const float2* __restrict__ means2D,
+                                                             const float* __restrict__ depths,
+                                                             const uint32_t* __restrict__ offsets,
+                                                             const int* __restrict__ radii, int grid_x, int grid_y,
+                                                             uint64_t* __restrict__ keys,
+                                                             uint32_t* __restrict__ gid_of_slot) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const int r = radii[idx];
+    if (r <= 0) return;
+    uint32_t off = idx == 0 ? 0u : offsets[idx - 1];
+    int x0, y0, x1, y1;
+    const float2 m = means2D[idx];
+    get_rect(m.x, m.y, r, grid_x, grid_y, x0, y0, x1, y1);
+    const uint64_t dbits = (uint64_t)__float_as_uint(depths[idx]);
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            keys[off] = ((uint64_t)(uint32_t)(y * grid_x + x) << 32) | dbits;
+            gid_of_slot[off] = (uint32_t)idx;
+            ++off;
+        }
+}
+
+// rasterizer_impl.cu:118-140 (identifyTileRanges), fused with the gather of sorted Gaussian ids.
+__global__ void __launch_bounds__(256) identify_ranges_kernel(int L, const uint64_t* __restrict__ keys,
+                                                              const uint32_t* __restrict__ sorted_slot,
+                                                              const uint32_t* __restrict__ gid_of_slot,
+                                                              uint32_t* __restrict__ point_list,
+                                                              uint2* __restrict__ ranges) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= L) return;
+    point_list[idx] = gid_of_slot[sorted_slot[idx]];
+    const uint32_t cur = (uint32_t)(keys[idx] >> 32);
+    if (idx == 0) {
+        ranges[cur].x = 0;
+    } else {
+        const uint32_t prev = (uint32_t)(keys[idx - 1] >> 32);
+        if (cur != prev) {
+            ranges[prev].y = idx;
+            ranges[cur].x = idx;
+        }
+    }
+    if (idx == L - 1) ranges[cur].y = L;
+}
+
+}  // namespace r3dg

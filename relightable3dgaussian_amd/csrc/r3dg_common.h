@@ -1,0 +1,157 @@
+// r3dg_common.h -- device-side constants, math helpers and the opaque state-buffer layouts
+// shared by the HIP kernels of the relightable splat rasterizer (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "r3dg_hip.h"
+
+namespace r3dg {
+
+constexpr int kTileX = 16;  // screen tile (reference config.h:15-16)
+constexpr int kTileY = 16;
+constexpr int kBlock = kTileX * kTileY;  // one pixel per thread, 4 wave64 per tile
+constexpr int kWave = 64;
+constexpr int kMaxFeatures = 32;  // S limit of this build (reference bwd caps S at 24, backward.cu:449)
+
+// Spherical-harmonic constants (reference auxiliary.h:22-39).
+__device__ constexpr float SH_C0 = 0.28209479177387814f;
+__device__ constexpr float SH_C1 = 0.4886025119029199f;
+__device__ constexpr float SH_C2_0 = 1.0925484305920792f;
+__device__ constexpr float SH_C2_1 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_2 = 0.31539156525252005f;
+__device__ constexpr float SH_C2_3 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_4 = 0.5462742152960396f;
+__device__ constexpr float SH_C3_0 = -0.5900435899266435f;
+__device__ constexpr float SH_C3_1 = 2.890611442640554f;
+__device__ constexpr float SH_C3_2 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_3 = 0.3731763325901154f;
+__device__ constexpr float SH_C3_4 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_5 = 1.445305721320277f;
+__device__ constexpr float SH_C3_6 = -0.5900435899266435f;
+
+// Feature output layout: channel c of pixel pix lives at a[c] + pix * m[c] (r3dg_feature_groups).
+struct FeatureLayout {
+    int a[kMaxFeatures];
+    int m[kMaxFeatures];
+};
+FeatureLayout make_feature_layout(int S, long long HW, bool native);
+
+// ---- opaque state buffers ------------------------------------------------------------------
+// Layouts are pure functions of (P), (L) and (H, W) so the backward can re-derive the pointers
+// from the buffers the autograd context kept (the reference does the same with fromChunk,
+// rasterizer_impl.cu:157-201). Every array starts on a 256-byte boundary.
+struct GeomState {
+    float* depths;          // [P]   view-space z
+    int* internal_radii;    // [P]   used when the caller passes no radii output
+    float2* means2D;        // [P]
+    float* cov3D;           // [P,6]
+    float4* conic_opacity;  // [P]
+    float* rgb;             // [P,3]
+    float* shader_rgb;      // [P,3] splat-shader colour (only written when a splat shader runs)
+    float* stencils;        // [P]
+    float* stencil_opacity; // [P]
+    uint8_t* clamped;       // [P] bit c: SH colour channel c clamped at 0
+    uint32_t* tiles_touched;// [P]
+    uint32_t* point_offsets;// [P] inclusive scan of tiles_touched
+    void* scan_temp;
+    size_t scan_temp_bytes;
+};
+struct BinningState {
+    uint64_t* keys_unsorted;  // [L] tile << 32 | float bits(depth)
+    uint64_t* keys_sorted;    // [L]
+    uint32_t* gid_of_slot;    // [L] Gaussian id of each unsorted (Gaussian-contiguous) slot
+    uint32_t* sorted_slot;    // [L] unsorted slot of each sorted instance (the sort permutation)
+    uint32_t* point_list;     // [L] Gaussian ids in sorted order (reference point_list)
+    void* sort_temp;
+    size_t sort_temp_bytes;
+};
+struct ImageState {
+    float* final_T;     // [H*W]
+    uint32_t* n_contrib;// [H*W]
+    uint2* ranges;      // [tiles]
+};
+
+size_t geom_state_bytes(size_t P);
+size_t binning_state_bytes(size_t L);
+size_t image_state_bytes(int H, int W);
+GeomState geom_state_from(void* base, size_t P);
+BinningState binning_state_from(void* base, size_t L);
+ImageState image_state_from(void* base, int H, int W);
+
+// ---- error handling --------------------------------------------------------------------------
+void set_error(const std::string& msg);
+
+#define R3DG_CHECK_HIP(expr)                                                                    \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess) {                                                                 \
+            ::r3dg::set_error(std::string(#expr) + ": " + hipGetErrorString(_e) + " at " +      \
+                              __FILE__ + ":" + std::to_string(__LINE__));                       \
+            return R3DG_ERR_HIP;                                                                \
+        }                                                                                       \
+    } while (0)
+
+#define R3DG_CHECK_LAUNCH(debug, stream)                                                        \
+    do {                                                                                        \
+        R3DG_CHECK_HIP(hipGetLastError());                                                      \
+        if (debug) R3DG_CHECK_HIP(hipStreamSynchronize(stream));                                \
+    } while (0)
+
+#define R3DG_REQUIRE(cond, msg)                                                                 \
+    do {                                                                                        \
+        if (!(cond)) {                                                                          \
+            ::r3dg::set_error(msg);                                                             \
+            return R3DG_ERR_ARG;                                                                \
+        }                                                                                       \
+    } while (0)
+
+// ---- device math -----------------------------------------------------------------------------
+__device__ __forceinline__ float ndc2pix(float v, int S) {
+    // auxiliary.h:41-44 evaluates in double (the literals are double)
+    return (float)((((double)v + 1.0) * S - 1.0) * 0.5);
+}
+
+__device__ __forceinline__ void get_rect(float px, float py, int max_radius, int gx, int gy, int& x0, int& y0,
+                                         int& x1, int& y1) {
+    // auxiliary.h:46-56
+    x0 = min(gx, max(0, (int)((px - (float)max_radius) / kTileX)));
+    y0 = min(gy, max(0, (int)((py - (float)max_radius) / kTileY)));
+    x1 = min(gx, max(0, (int)((px + (float)max_radius + kTileX - 1) / kTileX)));
+    y1 = min(gy, max(0, (int)((py + (float)max_radius + kTileY - 1) / kTileY)));
+}
+
+__device__ __forceinline__ float3 xform_point4x3(float3 p, const float* m) {
+    return make_float3(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+
+__device__ __forceinline__ float4 xform_point4x4(float3 p, const float* m) {
+    return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14], m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+}
+
+// Wave-wide sum over 64 lanes with DPP (result valid in lane 63).
+__device__ __forceinline__ float dpp_f(float v, int ctrl_dummy);
+
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF, bool BOUND = false>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, BANK_MASK, BOUND));
+}
+
+__device__ __forceinline__ float wave_sum_to_lane63(float v) {
+    v += dpp_mov<0xB1>(v);          // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);          // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141>(v);         // row_half_mirror
+    v += dpp_mov<0x140>(v);         // row_mirror        -> every lane: its 16-lane row sum
+    v += dpp_mov<0x142, 0xA>(v);    // row_bcast:15      -> rows 1,3 += row 0,2
+    v += dpp_mov<0x143, 0xC>(v);    // row_bcast:31      -> rows 2,3 += lane 31
+    return v;                       // lane 63 holds the total
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+}  // namespace r3dg

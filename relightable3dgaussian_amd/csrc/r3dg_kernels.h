@@ -1,0 +1,157 @@
+// r3dg_kernels.h -- kernel argument blocks and launch helpers shared between the kernel
+// translation units and the host orchestration (rasterizer.hip).
+#pragma once
+
+#include "r3dg_common.h"
+
+namespace r3dg {
+
+struct PreprocessArgs {
+    int P, D, M, W, H, grid_x, grid_y, prefiltered;
+    float focal_x, focal_y, tan_fovx, tan_fovy, scale_modifier;
+    const float* means3D;
+    const float* scales;
+    const float* rotations;
+    const float* opacity;
+    const float* sh;
+    const float* cov3D_precomp;
+    const float* colors_precomp;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    int* radii;
+    uint32_t* tiles_touched;
+    float* depths;
+    float2* means2D;
+    float* cov3D;
+    float4* conic_opacity;
+    float* rgb;
+    uint8_t* clamped;
+    unsigned int* error_flag;
+};
+
+struct RenderFwdArgs {
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float* depths;
+    const float* colors;
+    const float* shader_colors;
+    const float* features;
+    const float* bg;
+    int S, W, H, grid_x, num_tiles, cull;
+    float* final_T;
+    uint32_t* n_contrib;
+    float* out_color;
+    float* out_opacity;
+    float* out_depth;
+    float* out_feature;
+    float* out_shader_color;
+    FeatureLayout flay;
+};
+
+// Per-instance gradient row written by the backward blend: [mean2D x,y,z | conic x,y,w |
+// opacity | colour r,g,b | features 0..S-1 | pad], RS floats (multiple of 4).
+constexpr int kRowMean = 0, kRowConic = 3, kRowOpacity = 6, kRowColor = 7, kRowFeat = 10;
+__host__ __device__ inline int row_stride(int S) { return ((kRowFeat + S) + 3) & ~3; }
+
+struct RenderBwdArgs {
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const uint32_t* sorted_slot;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float* depths;
+    const float* colors;
+    const float* features;
+    const float* bg;
+    const float* final_T;
+    const uint32_t* n_contrib;
+    const float* dL_dpix;      // colour grads, channel c of pixel p at ca[c] + p * cm[c]
+    int ca[3], cm[3];
+    const float* dL_dpix_o;
+    const float* dL_dpix_d;
+    const float* dL_dpix_f;    // feature grads, layout gflay
+    FeatureLayout gflay;
+    int S, W, H, grid_x, num_tiles, cull, backward_geometry, RS;
+    float* rows;               // [L, RS]
+};
+
+struct GatherBwdArgs {
+    int P, D, M, S, RS;
+    const float* rows;
+    const uint32_t* offsets;
+    const int* radii;
+    const float* means3D;
+    const float* sh;
+    const uint8_t* clamped;
+    const float* scales;
+    const float* rotations;
+    float scale_modifier;
+    const float* cov3D;       // precomputed or geom-state cov3D
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float focal_x, focal_y, tan_fovx, tan_fovy;
+    int use_scales;           // scales/rotations given (cov3D not precomputed)
+    float* dL_dmeans2D;
+    float* dL_dcolors;
+    float* dL_dopacity;
+    float* dL_dmeans3D;
+    float* dL_dfeatures;
+    float* dL_dcov3D;
+    float* dL_dsh;
+    float* dL_dscales;
+    float* dL_drotations;
+};
+
+struct XyzNormalArgs {
+    int W, H;
+    const float* view;
+    float focal_x, focal_y, cx, cy;
+    const float* opacity;
+    const float* depth;
+    float* normal;
+    float* xyz;
+};
+
+struct IntermediateArgs {
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float* depths;
+    const float* stencils;
+    const float* stencil_opacity;
+    int W, H, grid_x, num_tiles;
+    float* out_depth;
+    float* out_stencil;
+};
+
+// kernels (defined in the .hip translation units)
+__global__ void preprocess_kernel(PreprocessArgs a);
+__global__ void mark_visible_kernel(int P, const float* means3D, const float* view, uint8_t* present);
+__global__ void duplicate_keys_kernel(int P, const float2* means2D, const float* depths, const uint32_t* offsets,
+                                      const int* radii, int grid_x, int grid_y, uint64_t* keys,
+                                      uint32_t* gid_of_slot);
+__global__ void identify_ranges_kernel(int L, const uint64_t* keys, const uint32_t* sorted_slot,
+                                       const uint32_t* gid_of_slot, uint32_t* point_list, uint2* ranges);
+__global__ void xyz_normal_kernel(XyzNormalArgs a);
+__global__ void intermediate_kernel(IntermediateArgs a);
+
+// host launchers for the templated blend kernels
+hipError_t launch_render_forward(const RenderFwdArgs& a, bool shader, hipStream_t stream);
+hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t stream);
+hipError_t launch_gather_backward(const GatherBwdArgs& a, hipStream_t stream);
+
+// XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so block b runs on the
+// same XCD as b+8. Give each XCD a contiguous band of tiles (neighbouring tiles share
+// Gaussians, so their attribute gathers hit the same L2). Grid is padded to a multiple of 8.
+__host__ __device__ inline int padded_tile_grid(int num_tiles) { return (num_tiles + 7) & ~7; }
+__device__ __forceinline__ int xcd_tile(int b, int grid) {
+    const int per = grid >> 3;
+    return (b & 7) * per + (b >> 3);
+}
+
+}  // namespace r3dg

@@ -1,0 +1,597 @@
+// rasterizer.hip -- host orchestration of the rasterizer and the C ABI (include/r3dg_hip.h).
+//
+// Restates CudaRasterizer::Rasterizer::forward / backward / markVisible
+// (reference rasterizer_impl.cu:143-639) on one HIP stream (the caller's), with:
+//   * no input clones when the SH shaders are the defaults (the reference clones six inputs
+//     every call, rasterize_points.cu:117-122, only so shaders may mutate them);
+//   * no RenderIntermediateTextures pass and no splat-shader launch when the splat shaders are
+//     the defaults (their only outputs are then a stencil of zeros and shader_rgb == rgb);
+//   * rocprim inclusive scan + stable LSD radix sort on bits [0, 32 + msb(tiles)) with the
+//     unsorted slot as the sorted value (see preprocess.hip duplicate_keys_kernel);
+//   * one blocking D2H read of num_rendered, as the reference (rasterizer_impl.cu:347).
+#include <cstring>  // before rocprim on ROCm 7.2
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "r3dg_common.h"
+#include "r3dg_kernels.h"
+
+namespace r3dg {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+static inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+FeatureLayout make_feature_layout(int S, long long HW, bool native) {
+    FeatureLayout f{};
+    int groups[kMaxFeatures];
+    const int ng = r3dg_feature_groups(S, groups);
+    int c = 0;
+    for (int gi = 0; gi < ng; ++gi)
+        for (int k = 0; k < groups[gi]; ++k, ++c) {
+            if (c >= kMaxFeatures) break;
+            if (native) {
+                f.a[c] = (int)(HW * (c - k) + k);
+                f.m[c] = groups[gi];
+            } else {  // planar [S, H, W]
+                f.a[c] = (int)(HW * c);
+                f.m[c] = 1;
+            }
+        }
+    return f;
+}
+
+// ---- state buffer layouts --------------------------------------------------------------------
+static size_t scan_temp_size(size_t P) {
+    size_t bytes = 0;
+    uint32_t* d = nullptr;
+    rocprim::inclusive_scan(nullptr, bytes, d, d, P, rocprim::plus<uint32_t>(), 0);
+    return bytes;
+}
+
+static size_t sort_temp_size(size_t L) {
+    size_t bytes = 0;
+    uint64_t* k = nullptr;
+    uint32_t* v = nullptr;
+    rocprim::radix_sort_pairs(nullptr, bytes, k, k, rocprim::counting_iterator<uint32_t>(0), v, L, 0, 64, 0);
+    return bytes;
+}
+
+// Carving works on an integer cursor so the same code computes sizes (base 0) and pointers.
+template <typename T>
+static T* carve(uintptr_t& p, size_t count) {
+    T* r = reinterpret_cast<T*>(p);
+    p += align256(sizeof(T) * count);
+    return r;
+}
+
+static GeomState carve_geom(uintptr_t p, size_t P, uintptr_t* end) {
+    GeomState g{};
+    g.depths = carve<float>(p, P);
+    g.internal_radii = carve<int>(p, P);
+    g.means2D = carve<float2>(p, P);
+    g.cov3D = carve<float>(p, 6 * P);
+    g.conic_opacity = carve<float4>(p, P);
+    g.rgb = carve<float>(p, 3 * P);
+    g.shader_rgb = carve<float>(p, 3 * P);
+    g.stencils = carve<float>(p, P);
+    g.stencil_opacity = carve<float>(p, P);
+    g.clamped = carve<uint8_t>(p, P);
+    g.tiles_touched = carve<uint32_t>(p, P);
+    g.point_offsets = carve<uint32_t>(p, P);
+    g.scan_temp_bytes = scan_temp_size(P);
+    g.scan_temp = carve<char>(p, g.scan_temp_bytes);
+    if (end) *end = p;
+    return g;
+}
+size_t geom_state_bytes(size_t P) {
+    uintptr_t end = 0;
+    carve_geom(0, P, &end);
+    return (size_t)end;
+}
+GeomState geom_state_from(void* base, size_t P) { return carve_geom((uintptr_t)base, P, nullptr); }
+
+static BinningState carve_binning(uintptr_t p, size_t L, uintptr_t* end) {
+    BinningState b{};
+    b.keys_unsorted = carve<uint64_t>(p, L);
+    b.keys_sorted = carve<uint64_t>(p, L);
+    b.gid_of_slot = carve<uint32_t>(p, L);
+    b.sorted_slot = carve<uint32_t>(p, L);
+    b.point_list = carve<uint32_t>(p, L);
+    b.sort_temp_bytes = sort_temp_size(L);
+    b.sort_temp = carve<char>(p, b.sort_temp_bytes);
+    if (end) *end = p;
+    return b;
+}
+size_t binning_state_bytes(size_t L) {
+    uintptr_t end = 0;
+    carve_binning(0, L, &end);
+    return (size_t)end + 256;
+}
+BinningState binning_state_from(void* base, size_t L) { return carve_binning((uintptr_t)base, L, nullptr); }
+
+static int num_tiles_of(int H, int W) { return ((W + kTileX - 1) / kTileX) * ((H + kTileY - 1) / kTileY); }
+
+static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end) {
+    ImageState s{};
+    const size_t N = (size_t)H * W;
+    s.final_T = carve<float>(p, N);
+    s.n_contrib = carve<uint32_t>(p, N);
+    s.ranges = carve<uint2>(p, (size_t)num_tiles_of(H, W));
+    if (end) *end = p;
+    return s;
+}
+size_t image_state_bytes(int H, int W) {
+    uintptr_t end = 0;
+    carve_image(0, H, W, &end);
+    return (size_t)end;
+}
+ImageState image_state_from(void* base, int H, int W) { return carve_image((uintptr_t)base, H, W, nullptr); }
+
+// rasterizer_impl.cu:37-52
+static uint32_t higher_msb(uint32_t n) {
+    uint32_t msb = sizeof(n) * 4, step = msb;
+    while (step > 1) {
+        step /= 2;
+        if (n >> msb) msb += step;
+        else msb -= step;
+    }
+    if (n >> msb) msb++;
+    return msb;
+}
+
+// ---- shader registry (ShShader.cu:196-230, splatShader.cu:283-333, postProcessShader.cu:395-436) ----
+// Handles are opaque ids: (kind + 1) << 32 | index into the alphabetically ordered name list
+// (the reference's ShaderManager iterates a std::map, i.e. in name order).
+static const std::vector<std::string>& shader_names(int kind) {
+    static const std::vector<std::string> sh = {"CullHalf", "ExpPos", "GaussDissolve", "Heartbeat", "ShDefault"};
+    static const std::vector<std::string> splat = {"Crack",         "CrackNoRecon",  "Dissolve",     "NaiveOutline",
+                                                   "QuantizeFlats", "QuantizeLight", "RoughnessOnly", "SplatDefault",
+                                                   "Stencil",       "Wireframe"};
+    static const std::vector<std::string> post = {"BlurLighting", "CrackReconstriction", "Invert",
+                                                  "Outline",      "QuantizeLighting",    "SobelFilter",
+                                                  "SplatDefault", "TexturedShadows",     "ToonShader"};
+    static const std::vector<std::string> none;
+    return kind == R3DG_SHADER_SH ? sh : kind == R3DG_SHADER_SPLAT ? splat : kind == R3DG_SHADER_POST ? post : none;
+}
+static int64_t make_handle(int kind, int idx) { return ((int64_t)(kind + 1) << 32) | (int64_t)idx; }
+static int handle_kind(int64_t h) { return (int)(h >> 32) - 1; }
+static int handle_index(int64_t h) { return (int)(h & 0xffffffff); }
+static int default_index(int kind) {
+    const auto& n = shader_names(kind);
+    const char* d = kind == R3DG_SHADER_SH ? "ShDefault" : "SplatDefault";
+    return (int)(std::find(n.begin(), n.end(), d) - n.begin());
+}
+
+struct ShaderManagerObj {
+    int kind;
+    std::vector<int> counts;       // per shader (name order)
+    std::vector<int*> d_lists;     // device splat-index list per shader
+    bool all_default;
+};
+static std::mutex g_mgr_mu;
+static std::map<int64_t, ShaderManagerObj*> g_managers;
+static int64_t g_next_mgr = 1;
+
+static ShaderManagerObj* lookup_manager(int64_t h) {
+    if (h == 0) return nullptr;
+    std::lock_guard<std::mutex> lk(g_mgr_mu);
+    auto it = g_managers.find(h);
+    return it == g_managers.end() ? nullptr : it->second;
+}
+
+static int build_manager(int kind, int P, const std::vector<int>& idx_per_splat, int64_t* out, hipStream_t st) {
+    const int n = (int)shader_names(kind).size();
+    auto* m = new ShaderManagerObj();
+    m->kind = kind;
+    m->counts.assign(n, 0);
+    std::vector<std::vector<int>> lists(n);
+    for (int i = 0; i < P; ++i) {
+        const int s = idx_per_splat[i];
+        if (s < 0 || s >= n) {
+            delete m;
+            set_error("shader manager: invalid shader index");
+            return R3DG_ERR_ARG;
+        }
+        lists[s].push_back(i);  // ascending splat order, as SortShadersCUDA (preprocessModel.cu:116-134)
+    }
+    m->all_default = true;
+    for (int s = 0; s < n; ++s) {
+        m->counts[s] = (int)lists[s].size();
+        int* d = nullptr;
+        if (!lists[s].empty()) {
+            R3DG_CHECK_HIP(hipMalloc(&d, sizeof(int) * lists[s].size()));
+            R3DG_CHECK_HIP(hipMemcpyAsync(d, lists[s].data(), sizeof(int) * lists[s].size(), hipMemcpyHostToDevice, st));
+            if (s != default_index(kind)) m->all_default = false;
+        }
+        m->d_lists.push_back(d);
+    }
+    R3DG_CHECK_HIP(hipStreamSynchronize(st));
+    std::lock_guard<std::mutex> lk(g_mgr_mu);
+    const int64_t h = (int64_t)0x5233000000000000ll | g_next_mgr++;
+    g_managers[h] = m;
+    *out = h;
+    return R3DG_OK;
+}
+
+// preprocessModel.cu:17-59 (SelectShadersCUDA): shader choice by splat position.
+__global__ void select_shaders_kernel(int P, const float* __restrict__ xyz, int8_t* sh_idx, int8_t* splat_idx,
+                                      int i_sh_default, int i_heartbeat, int i_gauss_dissolve, int i_splat_default,
+                                      int i_wireframe, int i_outline, int i_dissolve) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float x = xyz[3 * i], y = xyz[3 * i + 1];
+    sh_idx[i] = (int8_t)(y < -0.3f ? i_sh_default : (y > 0.4f ? i_heartbeat : i_gauss_dissolve));
+    int s;
+    if (x < -0.6f) s = i_splat_default;
+    else if (x > -0.6f && x < 0) s = i_wireframe;
+    else if (x > 0 && x < 0.5) s = i_outline;
+    else s = i_dissolve;
+    splat_idx[i] = (int8_t)s;
+}
+
+static int name_index(int kind, const char* name) {
+    const auto& n = shader_names(kind);
+    auto it = std::find(n.begin(), n.end(), std::string(name));
+    return it == n.end() ? -1 : (int)(it - n.begin());
+}
+
+}  // namespace r3dg
+
+using namespace r3dg;
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" int r3dg_abi_version(void) { return R3DG_ABI_VERSION; }
+extern "C" const char* r3dg_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int r3dg_feature_groups(int S, int* groups) {
+    int n = 0;
+    if (S == 21) {
+        const int g[9] = {1, 1, 1, 3, 3, 3, 3, 3, 3};
+        for (n = 0; n < 9; ++n) groups[n] = g[n];
+    } else if (S == 11) {
+        const int g[5] = {1, 1, 3, 3, 3};
+        for (n = 0; n < 5; ++n) groups[n] = g[n];
+    } else {
+        for (n = 0; n < S; ++n) groups[n] = 1;
+    }
+    return n;
+}
+
+extern "C" size_t r3dg_image_state_n_contrib_offset(int H, int W) { return align256(4 * (size_t)H * W); }
+
+extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3dg_gaussians* g,
+                                        const r3dg_forward_outputs* out, r3dg_alloc_fn geom_alloc, void* geom_ctx,
+                                        r3dg_alloc_fn binning_alloc, void* binning_ctx, r3dg_alloc_fn image_alloc,
+                                        void* image_ctx, int* num_rendered, r3dg_stream_t stream) {
+    hipStream_t st = (hipStream_t)stream;
+    R3DG_REQUIRE(s && g && out && num_rendered, "rasterize_gaussians: null argument");
+    const int P = s->P, S = s->S, H = s->H, W = s->W;
+    R3DG_REQUIRE(P >= 0 && H > 0 && W > 0, "rasterize_gaussians: invalid sizes");
+    R3DG_REQUIRE(S >= 0 && S <= kMaxFeatures, "rasterize_gaussians: at most 32 feature channels are supported");
+    R3DG_REQUIRE((g->colors_precomp != nullptr) != (g->sh != nullptr) || P == 0,
+                 "Please provide excatly one of either SHs or precomputed colors!");
+    R3DG_REQUIRE(((g->scales && g->rotations) != (g->cov3D_precomp != nullptr)) || P == 0,
+                 "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    R3DG_REQUIRE(S == 0 || P == 0 || g->features, "rasterize_gaussians: features missing");
+    R3DG_REQUIRE((long long)H * W * (S > 3 ? S : 3) < (1ll << 31), "rasterize_gaussians: image too large");
+    *num_rendered = 0;
+
+    // shaders: this build runs the default SH / splat shaders and no post-process passes
+    // (DESIGN.md "Scope"; the shader library is the next row of SURVEY.md §8f).
+    ShaderManagerObj* shm = lookup_manager(s->sh_shader_manager);
+    ShaderManagerObj* spm = lookup_manager(s->splat_shader_manager);
+    R3DG_REQUIRE(s->sh_shader_manager == 0 || shm, "rasterize_gaussians: unknown SH shader manager handle");
+    R3DG_REQUIRE(s->splat_shader_manager == 0 || spm, "rasterize_gaussians: unknown splat shader manager handle");
+    if ((shm && !shm->all_default) || (spm && !spm->all_default) || s->n_post_passes > 0) {
+        set_error("rasterize_gaussians: non-default SH/splat shaders and post-process passes are not in this "
+                  "build's scope yet (DESIGN.md 'Scope'); use default shaders (handle 0)");
+        return R3DG_ERR_UNSUPPORTED;
+    }
+
+    const int gx = (W + kTileX - 1) / kTileX, gy = (H + kTileY - 1) / kTileY;
+    const int T = gx * gy;
+    void* geom_base = geom_alloc(geom_ctx, geom_state_bytes((size_t)P));
+    void* img_base = image_alloc(image_ctx, image_state_bytes(H, W));
+    if (!geom_base || !img_base) {
+        set_error("rasterize_gaussians: state allocation failed");
+        return R3DG_ERR_ALLOC;
+    }
+    GeomState geom = geom_state_from(geom_base, (size_t)P);
+    ImageState img = image_state_from(img_base, H, W);
+    int* radii = out->radii ? out->radii : geom.internal_radii;
+    const float focal_y = H / (2.0f * s->tan_fovy);
+    const float focal_x = W / (2.0f * s->tan_fovx);
+
+    int L = 0;
+    if (P > 0) {
+        PreprocessArgs pa{};
+        pa.P = P; pa.D = s->D; pa.M = s->M; pa.W = W; pa.H = H; pa.grid_x = gx; pa.grid_y = gy;
+        pa.prefiltered = s->prefiltered;
+        pa.focal_x = focal_x; pa.focal_y = focal_y; pa.tan_fovx = s->tan_fovx; pa.tan_fovy = s->tan_fovy;
+        pa.scale_modifier = s->scale_modifier;
+        pa.means3D = g->means3D; pa.scales = g->scales; pa.rotations = g->rotations; pa.opacity = g->opacity;
+        pa.sh = g->sh; pa.cov3D_precomp = g->cov3D_precomp; pa.colors_precomp = g->colors_precomp;
+        pa.view = s->viewmatrix; pa.proj = s->projmatrix; pa.campos = s->campos;
+        pa.radii = radii; pa.tiles_touched = geom.tiles_touched; pa.depths = geom.depths;
+        pa.means2D = geom.means2D; pa.cov3D = geom.cov3D; pa.conic_opacity = geom.conic_opacity;
+        pa.rgb = geom.rgb; pa.clamped = geom.clamped; pa.error_flag = nullptr;
+        hipLaunchKernelGGL(preprocess_kernel, dim3((P + 255) / 256), dim3(256), 0, st, pa);
+        R3DG_CHECK_LAUNCH(s->debug, st);
+
+        size_t tb = geom.scan_temp_bytes;
+        R3DG_CHECK_HIP(rocprim::inclusive_scan(geom.scan_temp, tb, geom.tiles_touched, geom.point_offsets,
+                                               (size_t)P, rocprim::plus<uint32_t>(), st));
+        uint32_t Lh = 0;
+        R3DG_CHECK_HIP(hipMemcpyAsync(&Lh, geom.point_offsets + P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        R3DG_CHECK_HIP(hipStreamSynchronize(st));
+        R3DG_REQUIRE(Lh < (1u << 31), "rasterize_gaussians: too many tile instances");
+        L = (int)Lh;
+    }
+
+    void* bin_base = binning_alloc(binning_ctx, binning_state_bytes((size_t)L));
+    if (!bin_base) {
+        set_error("rasterize_gaussians: binning allocation failed");
+        return R3DG_ERR_ALLOC;
+    }
+    BinningState bin = binning_state_from(bin_base, (size_t)L);
+    R3DG_CHECK_HIP(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, st));
+    if (L > 0) {
+        hipLaunchKernelGGL(duplicate_keys_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, geom.means2D,
+                           geom.depths, geom.point_offsets, radii, gx, gy, bin.keys_unsorted, bin.gid_of_slot);
+        R3DG_CHECK_LAUNCH(s->debug, st);
+        const int bit = (int)higher_msb((uint32_t)T);
+        size_t sb = bin.sort_temp_bytes;
+        R3DG_CHECK_HIP(rocprim::radix_sort_pairs(bin.sort_temp, sb, bin.keys_unsorted, bin.keys_sorted,
+                                                 rocprim::counting_iterator<uint32_t>(0), bin.sorted_slot,
+                                                 (size_t)L, 0, 32 + bit, st));
+        hipLaunchKernelGGL(identify_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, st, L, bin.keys_sorted,
+                           bin.sorted_slot, bin.gid_of_slot, bin.point_list, img.ranges);
+        R3DG_CHECK_LAUNCH(s->debug, st);
+    }
+
+    // stencil: default shaders give all-zero stencil values (InitializeStencil, rasterizer_impl.cu:203-209)
+    if (out->stencil) R3DG_CHECK_HIP(hipMemsetAsync(out->stencil, 0, sizeof(float) * (size_t)H * W, st));
+
+    RenderFwdArgs ra{};
+    ra.ranges = img.ranges;
+    ra.point_list = bin.point_list;
+    ra.means2D = geom.means2D;
+    ra.conic_opacity = geom.conic_opacity;
+    ra.depths = geom.depths;
+    ra.colors = g->colors_precomp ? g->colors_precomp : geom.rgb;
+    ra.shader_colors = ra.colors;
+    ra.features = g->features;
+    ra.bg = s->bg;
+    ra.S = S; ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = T; ra.cull = 1;
+    ra.final_T = img.final_T;
+    ra.n_contrib = img.n_contrib;
+    ra.out_color = out->color;
+    ra.out_opacity = out->opacity;
+    ra.out_depth = out->depth;
+    ra.out_feature = out->feature;
+    ra.out_shader_color = out->shader_color;
+    ra.flay = make_feature_layout(S, (long long)H * W, true);
+    if (const char* e = getenv("R3DG_NO_CULL")) ra.cull = (e[0] == '0');
+    R3DG_CHECK_HIP(launch_render_forward(ra, false, st));
+    R3DG_CHECK_LAUNCH(s->debug, st);
+
+    if (s->compute_pseudo_normal) {
+        XyzNormalArgs xa{};
+        xa.W = W; xa.H = H; xa.view = s->viewmatrix; xa.focal_x = focal_x; xa.focal_y = focal_y;
+        xa.cx = s->cx; xa.cy = s->cy; xa.opacity = out->opacity; xa.depth = out->depth;
+        xa.normal = out->normal; xa.xyz = out->surface_xyz;
+        hipLaunchKernelGGL(xyz_normal_kernel, dim3(gx, gy), dim3(256), 0, st, xa);
+        R3DG_CHECK_LAUNCH(s->debug, st);
+    } else {
+        if (out->normal) R3DG_CHECK_HIP(hipMemsetAsync(out->normal, 0, sizeof(float) * 3 * (size_t)H * W, st));
+        if (out->surface_xyz)
+            R3DG_CHECK_HIP(hipMemsetAsync(out->surface_xyz, 0, sizeof(float) * 3 * (size_t)H * W, st));
+    }
+    *num_rendered = L;
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_state_view(int P, int H, int W, int L, void* geom, void* binning, void* image,
+                               r3dg_binning_view* v) {
+    R3DG_REQUIRE(v, "state_view: null");
+    GeomState gs = geom_state_from(geom, (size_t)P);
+    BinningState bs = binning_state_from(binning, (size_t)L);
+    ImageState is = image_state_from(image, H, W);
+    v->keys_sorted = bs.keys_sorted;
+    v->point_list = bs.point_list;
+    v->ranges = reinterpret_cast<const uint32_t*>(is.ranges);
+    v->point_offsets = gs.point_offsets;
+    v->depths = gs.depths;
+    v->means2D = reinterpret_cast<const float*>(gs.means2D);
+    v->conic_opacity = reinterpret_cast<const float*>(gs.conic_opacity);
+    v->rgb = gs.rgb;
+    v->cov3D = gs.cov3D;
+    v->clamped = gs.clamped;
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, const r3dg_gaussians* g,
+                                                 const int* radii_in, const r3dg_backward_grads* gr, void* geom,
+                                                 void* binning, void* image, int num_rendered,
+                                                 int backward_geometry, r3dg_alloc_fn scratch_alloc,
+                                                 void* scratch_ctx, const r3dg_backward_outputs* out,
+                                                 r3dg_stream_t stream) {
+    hipStream_t st = (hipStream_t)stream;
+    R3DG_REQUIRE(s && g && gr && out, "rasterize_gaussians_backward: null argument");
+    const int P = s->P, S = s->S, H = s->H, W = s->W, L = num_rendered;
+    R3DG_REQUIRE(P >= 0 && L >= 0 && S >= 0 && S <= kMaxFeatures, "rasterize_gaussians_backward: invalid sizes");
+    if (P == 0) return R3DG_OK;
+    const int gx = (W + kTileX - 1) / kTileX, gy = (H + kTileY - 1) / kTileY;
+    const int T = gx * gy;
+    GeomState gs = geom_state_from(geom, (size_t)P);
+    BinningState bs = binning_state_from(binning, (size_t)L);
+    ImageState is = image_state_from(image, H, W);
+    const int* radii = radii_in ? radii_in : gs.internal_radii;
+    const int RS = row_stride(S);
+    float* rows = nullptr;
+    if (L > 0) {
+        rows = (float*)scratch_alloc(scratch_ctx, sizeof(float) * (size_t)RS * L);
+        if (!rows) {
+            set_error("rasterize_gaussians_backward: scratch allocation failed");
+            return R3DG_ERR_ALLOC;
+        }
+        RenderBwdArgs ba{};
+        ba.ranges = is.ranges;
+        ba.point_list = bs.point_list;
+        ba.sorted_slot = bs.sorted_slot;
+        ba.means2D = gs.means2D;
+        ba.conic_opacity = gs.conic_opacity;
+        ba.depths = gs.depths;
+        ba.colors = g->colors_precomp ? g->colors_precomp : gs.rgb;
+        ba.features = g->features;
+        ba.bg = s->bg;
+        ba.final_T = is.final_T;
+        ba.n_contrib = is.n_contrib;
+        ba.dL_dpix = gr->dL_dout_color;
+        const long long HW = (long long)H * W;
+        for (int c = 0; c < 3; ++c) {
+            ba.ca[c] = gr->color_hwc ? c : (int)(c * HW);
+            ba.cm[c] = gr->color_hwc ? 3 : 1;
+        }
+        ba.dL_dpix_o = gr->dL_dout_opacity;
+        ba.dL_dpix_d = gr->dL_dout_depth;
+        ba.dL_dpix_f = gr->dL_dout_feature;
+        ba.gflay = make_feature_layout(S, HW, gr->feature_native != 0);
+        ba.S = S; ba.W = W; ba.H = H; ba.grid_x = gx; ba.num_tiles = T; ba.cull = 1;
+        if (const char* e = getenv("R3DG_NO_CULL")) ba.cull = (e[0] == '0');
+        ba.backward_geometry = backward_geometry;
+        ba.RS = RS;
+        ba.rows = rows;
+        R3DG_CHECK_HIP(launch_render_backward(ba, st));
+        R3DG_CHECK_LAUNCH(s->debug, st);
+    }
+    GatherBwdArgs ga{};
+    ga.P = P; ga.D = s->D; ga.M = s->M; ga.S = S; ga.RS = RS;
+    ga.rows = rows;
+    ga.offsets = gs.point_offsets;
+    ga.radii = radii;
+    ga.means3D = g->means3D;
+    ga.sh = g->sh;
+    ga.clamped = gs.clamped;
+    ga.scales = g->scales;
+    ga.rotations = g->rotations;
+    ga.scale_modifier = s->scale_modifier;
+    ga.cov3D = g->cov3D_precomp ? g->cov3D_precomp : gs.cov3D;
+    ga.view = s->viewmatrix;
+    ga.proj = s->projmatrix;
+    ga.campos = s->campos;
+    ga.focal_x = W / (2.0f * s->tan_fovx);
+    ga.focal_y = H / (2.0f * s->tan_fovy);
+    ga.tan_fovx = s->tan_fovx;
+    ga.tan_fovy = s->tan_fovy;
+    ga.use_scales = (g->scales != nullptr && g->cov3D_precomp == nullptr);
+    ga.dL_dmeans2D = out->dL_dmeans2D;
+    ga.dL_dcolors = out->dL_dcolors;
+    ga.dL_dopacity = out->dL_dopacity;
+    ga.dL_dmeans3D = out->dL_dmeans3D;
+    ga.dL_dfeatures = out->dL_dfeatures;
+    ga.dL_dcov3D = out->dL_dcov3D;
+    ga.dL_dsh = (s->M > 0) ? out->dL_dsh : nullptr;
+    ga.dL_dscales = out->dL_dscales;
+    ga.dL_drotations = out->dL_drotations;
+    if (!g->sh) ga.sh = nullptr;
+    R3DG_CHECK_HIP(launch_gather_backward(ga, st));
+    R3DG_CHECK_LAUNCH(s->debug, st);
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                                 uint8_t* present, r3dg_stream_t stream) {
+    (void)projmatrix;
+    if (P <= 0) return R3DG_OK;
+    hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, means3D,
+                       viewmatrix, present);
+    R3DG_CHECK_HIP(hipGetLastError());
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_shader_count(int kind) { return (int)shader_names(kind).size(); }
+extern "C" const char* r3dg_shader_name(int kind, int index) {
+    const auto& n = shader_names(kind);
+    return (index >= 0 && index < (int)n.size()) ? n[index].c_str() : nullptr;
+}
+extern "C" int64_t r3dg_shader_handle(int kind, int index) {
+    const auto& n = shader_names(kind);
+    return (index >= 0 && index < (int)n.size()) ? make_handle(kind, index) : 0;
+}
+
+extern "C" int r3dg_preprocess_model(int P, const float* xyz, int64_t* sh_manager, int64_t* splat_manager,
+                                     r3dg_stream_t stream) {
+    hipStream_t st = (hipStream_t)stream;
+    R3DG_REQUIRE(P >= 0 && sh_manager && splat_manager, "PreprocessModel: invalid arguments");
+    std::vector<int8_t> hs(P), hp(P);
+    if (P > 0) {
+        int8_t *ds = nullptr, *dp = nullptr;
+        R3DG_CHECK_HIP(hipMalloc(&ds, P));
+        R3DG_CHECK_HIP(hipMalloc(&dp, P));
+        hipLaunchKernelGGL(select_shaders_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, xyz, ds, dp,
+                           name_index(R3DG_SHADER_SH, "ShDefault"), name_index(R3DG_SHADER_SH, "Heartbeat"),
+                           name_index(R3DG_SHADER_SH, "GaussDissolve"), name_index(R3DG_SHADER_SPLAT, "SplatDefault"),
+                           name_index(R3DG_SHADER_SPLAT, "Wireframe"), name_index(R3DG_SHADER_SPLAT, "NaiveOutline"),
+                           name_index(R3DG_SHADER_SPLAT, "Dissolve"));
+        R3DG_CHECK_HIP(hipGetLastError());
+        R3DG_CHECK_HIP(hipMemcpyAsync(hs.data(), ds, P, hipMemcpyDeviceToHost, st));
+        R3DG_CHECK_HIP(hipMemcpyAsync(hp.data(), dp, P, hipMemcpyDeviceToHost, st));
+        R3DG_CHECK_HIP(hipStreamSynchronize(st));
+        R3DG_CHECK_HIP(hipFree(ds));
+        R3DG_CHECK_HIP(hipFree(dp));
+    }
+    std::vector<int> is(hs.begin(), hs.end()), ip(hp.begin(), hp.end());
+    int rc = build_manager(R3DG_SHADER_SH, P, is, sh_manager, st);
+    if (rc) return rc;
+    return build_manager(R3DG_SHADER_SPLAT, P, ip, splat_manager, st);
+}
+
+extern "C" int r3dg_create_shader_manager(int kind, int P, const int64_t* handles, int64_t* manager,
+                                          r3dg_stream_t stream) {
+    R3DG_REQUIRE(kind == R3DG_SHADER_SH || kind == R3DG_SHADER_SPLAT, "create_shader_manager: bad kind");
+    R3DG_REQUIRE(P >= 0 && manager && (P == 0 || handles), "create_shader_manager: invalid arguments");
+    std::vector<int> idx(P);
+    for (int i = 0; i < P; ++i) {
+        R3DG_REQUIRE(handle_kind(handles[i]) == kind, "create_shader_manager: handle of the wrong shader kind");
+        idx[i] = handle_index(handles[i]);
+    }
+    return build_manager(kind, P, idx, manager, (hipStream_t)stream);
+}
+
+extern "C" int r3dg_shader_manager_info(int64_t manager, int* n_shaders, int64_t* handles, int* counts) {
+    ShaderManagerObj* m = lookup_manager(manager);
+    R3DG_REQUIRE(m, "shader_manager_info: unknown handle");
+    const int n = (int)m->counts.size();
+    if (n_shaders) *n_shaders = n;
+    for (int i = 0; i < n; ++i) {
+        if (handles) handles[i] = make_handle(m->kind, i);
+        if (counts) counts[i] = m->counts[i];
+    }
+    return R3DG_OK;
+}
+
+// utils/texture.cu:33-76
+extern "C" int r3dg_encode_texture_mode(const char* mode) {
+    static const char* names[] = {"1", "L", "P", "RGB", "RGBA", "CMYK", "YCbCr", "LAB", "HSV", "I", "F"};
+    for (int i = 0; i < 11; ++i)
+        if (mode && strcmp(mode, names[i]) == 0) return i;
+    return -1;
+}
+extern "C" int r3dg_encode_wrap_mode(const char* mode) {
+    if (!mode) return -1;
+    if (!strcmp(mode, "Border")) return (int)hipAddressModeBorder;
+    if (!strcmp(mode, "Clamp")) return (int)hipAddressModeClamp;
+    if (!strcmp(mode, "Mirror")) return (int)hipAddressModeMirror;
+    if (!strcmp(mode, "Wrap")) return (int)hipAddressModeWrap;
+    return -1;
+}

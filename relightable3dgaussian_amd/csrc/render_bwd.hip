@@ -1,0 +1,519 @@
+// render_bwd.hip -- backward of the tile blend and of the per-Gaussian preprocessing (gfx950).
+//
+// Restates reference backward.cu:401-614 (renderCUDA backward), :144-276 (computeCov2DCUDA),
+// :20-139 (SH backward), :280-343 (cov3D backward), :348-398 (preprocessCUDA backward).
+//
+// MI355X design (replaces the reference's per-pixel float atomicAdd scatter, ~(10+S) atomics
+// per contributing pixel, backward.cu:552-611):
+//   1. render_bwd_kernel: one workgroup per tile replays the tile's list back to front. For each
+//      instance every wave reduces its 64 pixels' contributions with DPP (6 VALU ops per value,
+//      no LDS traffic) and lane 63 stores the wave total in the wave's own LDS partial row; per
+//      chunk of 64 instances the block sums the four wave partials in a fixed order and writes
+//      ONE gradient row per (tile, Gaussian) instance with plain vector stores -- at the
+//      instance's unsorted slot, which the sort permutation gives us. Slots are
+//      Gaussian-contiguous (duplicateWithKeys order).
+//   2. gather_bwd_kernel: one thread per Gaussian sums its contiguous rows in a fixed order,
+//      then runs the cov2D / projection / SH / cov3D backward for that Gaussian. No global
+//      atomics anywhere; the result is bitwise reproducible run to run (the reference's is not).
+#include "r3dg_common.h"
+#include "r3dg_kernels.h"
+
+namespace r3dg {
+
+__device__ __forceinline__ uint32_t quadrant_mask_b(float2 xy, float4 co, int x0, int y0, int cull) {
+    // identical test to render_fwd.hip quadrant_mask (see the derivation there)
+    if (!cull) return 0xFu;
+    if (co.w < 1.0f / 255.0f) return 0u;
+    const float det = co.x * co.z - co.y * co.y;
+    if (!(det > 0.0f)) return 0xFu;
+    const float t = 2.0f * __logf(255.0f * co.w) * 1.1f + 0.1f;
+    const float ex = sqrtf(t * co.z / det) + 1.0f;
+    const float ey = sqrtf(t * co.x / det) + 1.0f;
+    if (!(ex < 1e30f) || !(ey < 1e30f)) return 0xFu;
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float qx = (float)(x0 + (q & 1) * 8), qy = (float)(y0 + (q >> 1) * 8);
+        if (xy.x + ex >= qx && xy.x - ex <= qx + 7.0f && xy.y + ey >= qy && xy.y - ey <= qy + 7.0f) m |= 1u << q;
+    }
+    return m;
+}
+
+__device__ __forceinline__ int wave_max_int(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+template <int SMAX>
+__global__ void __launch_bounds__(kBlock) render_bwd_kernel(RenderBwdArgs a) {
+    constexpr int NA4 = (4 + SMAX + 3) / 4;      // attribute row: colour, depth, features
+    constexpr int NR = kRowFeat + SMAX;          // reduced values per instance
+    constexpr int RSL = (NR + 3) & ~3;           // LDS partial row stride (floats)
+    constexpr int CH = 64;                       // instances per flush chunk
+    __shared__ float2 s_xy[kBlock];
+    __shared__ float4 s_co[kBlock];
+    __shared__ uint32_t s_mask[kBlock];
+    __shared__ uint32_t s_slot[kBlock];
+    __shared__ float4 s_attr[kBlock * NA4];
+    __shared__ float4 s_part4[4 * CH * RSL / 4];  // [wave][chunk instance][RSL]
+    __shared__ int s_max_last;
+    float* s_part = reinterpret_cast<float*>(s_part4);
+
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (tile >= a.num_tiles) return;
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
+    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const int pix = inside ? py * a.W + px : 0;
+    const float pfx = (float)px, pfy = (float)py;
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+
+    const float T_final = inside ? a.final_T[pix] : 0.f;
+    float T = T_final;
+    const int last = inside ? (int)a.n_contrib[pix] : 0;
+    float g[3], gf[SMAX > 0 ? SMAX : 1], gd = 0.f, go = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) g[c] = inside ? a.dL_dpix[a.ca[c] + pix * a.cm[c]] : 0.f;
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c)
+        gf[c] = (inside && c < a.S) ? a.dL_dpix_f[a.gflay.a[c] + pix * a.gflay.m[c]] : 0.f;
+    if (inside) {
+        gd = a.dL_dpix_d[pix];
+        go = a.dL_dpix_o[pix];
+    }
+    const float bg_dot = a.bg[0] * g[0] + a.bg[1] * g[1] + a.bg[2] * g[2];
+    const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
+
+    float acc[3] = {0.f, 0.f, 0.f}, acc_f[SMAX > 0 ? SMAX : 1], acc_d = 0.f, acc_o = 0.f;
+    float last_alpha = 0.f, last_depth = 0.f, last_color[3] = {0.f, 0.f, 0.f}, last_f[SMAX > 0 ? SMAX : 1];
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c) {
+        acc_f[c] = 0.f;
+        last_f[c] = 0.f;
+    }
+
+    // Positions >= max(n_contrib) over the tile are never blended: their rows are zero.
+    const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
+    if (t == 0) s_max_last = 0;
+    for (int i = t; i < 4 * CH * RSL / 4; i += kBlock) s_part4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    if (l == 0) atomicMax(&s_max_last, wmax);
+    __syncthreads();
+    const int max_last = s_max_last;
+    const int RS = a.RS;
+    for (int p = max_last + t; p < n; p += kBlock) {
+        float4* row = reinterpret_cast<float4*>(a.rows + (size_t)a.sorted_slot[range.x + p] * RS);
+        for (int q = 0; q < RS / 4; ++q) row[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+
+    for (int hi = max_last; hi > 0; hi -= kBlock) {
+        const int cnt = min(kBlock, hi);
+        __syncthreads();  // previous batch fully consumed before the staging arrays are reused
+        if (t < cnt) {
+            const uint32_t k = range.x + (uint32_t)(hi - 1 - t);
+            const uint32_t gid = a.point_list[k];
+            s_slot[t] = a.sorted_slot[k];
+            const float2 xy = a.means2D[gid];
+            const float4 co = a.conic_opacity[gid];
+            s_xy[t] = xy;
+            s_co[t] = co;
+            s_mask[t] = quadrant_mask_b(xy, co, tx * kTileX, ty * kTileY, a.cull);
+            float v[NA4 * 4];
+#pragma unroll
+            for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
+            v[0] = a.colors[3 * gid + 0];
+            v[1] = a.colors[3 * gid + 1];
+            v[2] = a.colors[3 * gid + 2];
+            v[3] = a.depths[gid];
+            const float* f = a.features + (size_t)gid * a.S;
+#pragma unroll
+            for (int c = 0; c < SMAX; ++c)
+                if (c < a.S) v[4 + c] = f[c];
+#pragma unroll
+            for (int q = 0; q < NA4; ++q)
+                s_attr[t * NA4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        }
+        __syncthreads();
+        for (int j0 = 0; j0 < cnt; j0 += CH) {
+            const int jn = min(CH, cnt - j0);
+            for (int jj = 0; jj < jn; ++jj) {
+                const int j = j0 + jj;
+                const int p = hi - 1 - j;  // position in the tile range (reference `contributor`)
+                if (p >= wmax) continue;   // no pixel of this wave reaches this far back
+                const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
+                if (!((m >> w) & 1u)) continue;
+                bool contrib = inside && p < last;
+                float G = 0.f, alpha = 0.f, dx = 0.f, dy = 0.f;
+                float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (contrib) {
+                    const float2 xy = s_xy[j];
+                    co = s_co[j];
+                    dx = xy.x - pfx;
+                    dy = xy.y - pfy;
+                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    if (power > 0.0f) {
+                        contrib = false;
+                    } else {
+                        G = __expf(power);
+                        alpha = fminf(0.99f, co.w * G);
+                        if (alpha < 1.0f / 255.0f) contrib = false;
+                    }
+                }
+                if (__ballot(contrib) == 0ull) continue;
+                float vals[NR];
+#pragma unroll
+                for (int r = 0; r < NR; ++r) vals[r] = 0.f;
+                if (contrib) {
+                    T = T / (1.f - alpha);
+                    const float dchannel_dcolor = alpha * T;
+                    float v[NA4 * 4];
+#pragma unroll
+                    for (int q = 0; q < NA4; ++q) {
+                        const float4 r = s_attr[j * NA4 + q];
+                        v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
+                    }
+                    float dL_dalpha = 0.0f;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        acc[c] = last_alpha * last_color[c] + (1.f - last_alpha) * acc[c];
+                        last_color[c] = v[c];
+                        dL_dalpha += (v[c] - acc[c]) * g[c];
+                        vals[kRowColor + c] = dchannel_dcolor * g[c];
+                    }
+#pragma unroll
+                    for (int c = 0; c < SMAX; ++c) {
+                        acc_f[c] = last_alpha * last_f[c] + (1.f - last_alpha) * acc_f[c];
+                        last_f[c] = v[4 + c];
+                        if (a.backward_geometry) dL_dalpha += (v[4 + c] - acc_f[c]) * gf[c];
+                        vals[kRowFeat + c] = dchannel_dcolor * gf[c];
+                    }
+                    acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
+                    last_depth = v[3];
+                    dL_dalpha += (v[3] - acc_d) * gd;
+                    acc_o = last_alpha + (1.f - last_alpha) * acc_o;
+                    dL_dalpha += (1.0f - acc_o) * go;
+                    dL_dalpha *= T;
+                    last_alpha = alpha;
+                    dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+                    const float dL_dG = co.w * dL_dalpha;
+                    const float gdx = G * dx, gdy = G * dy;
+                    const float dG_ddelx = -gdx * co.x - gdy * co.y;
+                    const float dG_ddely = -gdy * co.z - gdx * co.y;
+                    vals[kRowMean + 0] = dL_dG * dG_ddelx * ddelx_dx;
+                    vals[kRowMean + 1] = dL_dG * dG_ddely * ddely_dy;
+                    vals[kRowMean + 2] = gd * dchannel_dcolor;
+                    vals[kRowConic + 0] = -0.5f * gdx * dx * dL_dG;
+                    vals[kRowConic + 1] = -0.5f * gdx * dy * dL_dG;
+                    vals[kRowConic + 2] = -0.5f * gdy * dy * dL_dG;
+                    vals[kRowOpacity] = G * dL_dalpha;
+                }
+                // wave totals (full exec mask here: the jj loop is wave-uniform)
+                float* dst = s_part + (w * CH + jj) * RSL;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    if (r < kRowFeat + a.S) {
+                        const float sum = wave_sum_to_lane63(vals[r]);
+                        if (l == 63) dst[r] = sum;
+                    }
+                }
+            }
+            __syncthreads();
+            // fixed-order sum of the four wave partials -> one row per instance; re-zero
+            for (int i = t; i < jn * (RS / 4); i += kBlock) {
+                const int jj = i / (RS / 4), q = i - jj * (RS / 4);
+                float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int ww = 0; ww < 4; ++ww) {
+                    float4* src = s_part4 + ((ww * CH + jj) * RSL) / 4 + q;
+                    const float4 v = *src;
+                    acc4.x += v.x; acc4.y += v.y; acc4.z += v.z; acc4.w += v.w;
+                    *src = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                reinterpret_cast<float4*>(a.rows + (size_t)s_slot[j0 + jj] * RS)[q] = acc4;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int SMAX>
+static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL((render_bwd_kernel<SMAX>), dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t stream) {
+    if (a.num_tiles == 0) return hipSuccess;
+    if (a.S == 0) return launch_bwd_s<0>(a, stream);
+    if (a.S <= 4) return launch_bwd_s<4>(a, stream);
+    if (a.S <= 8) return launch_bwd_s<8>(a, stream);
+    if (a.S <= 12) return launch_bwd_s<12>(a, stream);
+    if (a.S <= 16) return launch_bwd_s<16>(a, stream);
+    if (a.S <= 24) return launch_bwd_s<24>(a, stream);
+    return launch_bwd_s<32>(a, stream);
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-Gaussian: sum of gradient rows + preprocessing backward
+// ---------------------------------------------------------------------------------------------
+
+// backward.cu:20-139 (computeColorFromSH backward). dL_dRGB already clamp-masked.
+__device__ static void sh_backward(int deg, int M, float3 pos, const float* campos, const float* sh,
+                                   const float* dRGB, float* dL_dmean, float* dsh) {
+    const float dox = pos.x - campos[0], doy = pos.y - campos[1], doz = pos.z - campos[2];
+    const float len = sqrtf(dox * dox + doy * doy + doz * doz);
+    const float x = dox / len, y = doy / len, z = doz / len;
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    float ddx[3] = {0.f, 0.f, 0.f}, ddy[3] = {0.f, 0.f, 0.f}, ddz[3] = {0.f, 0.f, 0.f};
+    float b[16];
+    b[0] = SH_C0;
+    b[1] = -SH_C1 * y; b[2] = SH_C1 * z; b[3] = -SH_C1 * x;
+    b[4] = SH_C2_0 * xy; b[5] = SH_C2_1 * yz; b[6] = SH_C2_2 * (2.f * zz - xx - yy); b[7] = SH_C2_3 * xz;
+    b[8] = SH_C2_4 * (xx - yy);
+    b[9] = SH_C3_0 * y * (3.f * xx - yy); b[10] = SH_C3_1 * xy * z; b[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
+    b[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy); b[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
+    b[14] = SH_C3_5 * z * (xx - yy); b[15] = SH_C3_6 * x * (xx - 3.f * yy);
+    const int ncoef = deg > 2 ? 16 : (deg > 1 ? 9 : (deg > 0 ? 4 : 1));
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dsh[3 * i + c] = i < ncoef ? b[i] * dRGB[c] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        if (deg > 0) {
+            ddx[c] = -SH_C1 * sh[3 * 3 + c];
+            ddy[c] = -SH_C1 * sh[1 * 3 + c];
+            ddz[c] = SH_C1 * sh[2 * 3 + c];
+            if (deg > 1) {
+                ddx[c] += SH_C2_0 * y * sh[4 * 3 + c] + SH_C2_2 * 2.f * -x * sh[6 * 3 + c] +
+                          SH_C2_3 * z * sh[7 * 3 + c] + SH_C2_4 * 2.f * x * sh[8 * 3 + c];
+                ddy[c] += SH_C2_0 * x * sh[4 * 3 + c] + SH_C2_1 * z * sh[5 * 3 + c] +
+                          SH_C2_2 * 2.f * -y * sh[6 * 3 + c] + SH_C2_4 * 2.f * -y * sh[8 * 3 + c];
+                ddz[c] += SH_C2_1 * y * sh[5 * 3 + c] + SH_C2_2 * 2.f * 2.f * z * sh[6 * 3 + c] +
+                          SH_C2_3 * x * sh[7 * 3 + c];
+                if (deg > 2) {
+                    ddx[c] += (SH_C3_0 * sh[9 * 3 + c] * 3.f * 2.f * xy + SH_C3_1 * sh[10 * 3 + c] * yz +
+                               SH_C3_2 * sh[11 * 3 + c] * -2.f * xy + SH_C3_3 * sh[12 * 3 + c] * -3.f * 2.f * xz +
+                               SH_C3_4 * sh[13 * 3 + c] * (-3.f * xx + 4.f * zz - yy) +
+                               SH_C3_5 * sh[14 * 3 + c] * 2.f * xz + SH_C3_6 * sh[15 * 3 + c] * 3.f * (xx - yy));
+                    ddy[c] += (SH_C3_0 * sh[9 * 3 + c] * 3.f * (xx - yy) + SH_C3_1 * sh[10 * 3 + c] * xz +
+                               SH_C3_2 * sh[11 * 3 + c] * (-3.f * yy + 4.f * zz - xx) +
+                               SH_C3_3 * sh[12 * 3 + c] * -3.f * 2.f * yz + SH_C3_4 * sh[13 * 3 + c] * -2.f * xy +
+                               SH_C3_5 * sh[14 * 3 + c] * -2.f * yz + SH_C3_6 * sh[15 * 3 + c] * -3.f * 2.f * xy);
+                    ddz[c] += (SH_C3_1 * sh[10 * 3 + c] * xy + SH_C3_2 * sh[11 * 3 + c] * 4.f * 2.f * yz +
+                               SH_C3_3 * sh[12 * 3 + c] * 3.f * (2.f * zz - xx - yy) +
+                               SH_C3_4 * sh[13 * 3 + c] * 4.f * 2.f * xz + SH_C3_5 * sh[14 * 3 + c] * (xx - yy));
+                }
+            }
+        }
+    }
+    const float dvx = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
+    const float dvy = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
+    const float dvz = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
+    // dnormvdv (auxiliary.h:107-117)
+    const float sum2 = dox * dox + doy * doy + doz * doz;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    dL_dmean[0] += ((+sum2 - dox * dox) * dvx - doy * dox * dvy - doz * dox * dvz) * invsum32;
+    dL_dmean[1] += (-dox * doy * dvx + (sum2 - doy * doy) * dvy - doz * doy * dvz) * invsum32;
+    dL_dmean[2] += (-dox * doz * dvx - doy * doz * dvy + (sum2 - doz * doz) * dvz) * invsum32;
+}
+
+// backward.cu:280-343 (gradient w.r.t. the un-normalised quaternion, as the reference)
+__device__ static void cov3d_backward(float3 sc, float mod, float4 q, const float* d, float* dscale, float* drot) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    float R[3][3];
+    R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y + r * z); R[0][2] = 2.f * (x * z - r * y);
+    R[1][0] = 2.f * (x * y - r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z + r * x);
+    R[2][0] = 2.f * (x * z + r * y); R[2][1] = 2.f * (y * z - r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+    const float s[3] = {mod * sc.x, mod * sc.y, mod * sc.z};
+    float M[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) M[i][j] = s[i] * R[i][j];
+    const float Dm[3][3] = {{d[0], 0.5f * d[1], 0.5f * d[2]}, {0.5f * d[1], d[3], 0.5f * d[4]},
+                            {0.5f * d[2], 0.5f * d[4], d[5]}};
+    float dM[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) dM[i][j] = 2.0f * (M[i][0] * Dm[0][j] + M[i][1] * Dm[1][j] + M[i][2] * Dm[2][j]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dscale[i] = R[i][0] * dM[i][0] + R[i][1] * dM[i][1] + R[i][2] * dM[i][2];
+    float E[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) E[i][j] = dM[i][j] * s[i];
+    drot[0] = 2 * z * (E[0][1] - E[1][0]) + 2 * y * (E[2][0] - E[0][2]) + 2 * x * (E[1][2] - E[2][1]);
+    drot[1] = 2 * y * (E[1][0] + E[0][1]) + 2 * z * (E[2][0] + E[0][2]) + 2 * r * (E[1][2] - E[2][1]) -
+              4 * x * (E[2][2] + E[1][1]);
+    drot[2] = 2 * x * (E[1][0] + E[0][1]) + 2 * r * (E[2][0] - E[0][2]) + 2 * z * (E[1][2] + E[2][1]) -
+              4 * y * (E[2][2] + E[0][0]);
+    drot[3] = 2 * r * (E[0][1] - E[1][0]) + 2 * x * (E[2][0] + E[0][2]) + 2 * y * (E[1][2] + E[2][1]) -
+              4 * z * (E[1][1] + E[0][0]);
+}
+
+template <int SMAX>
+__global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
+    constexpr int NR = kRowFeat + SMAX;
+    constexpr int NQ = (NR + 3) / 4;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.P) return;
+    const uint32_t start = g == 0 ? 0u : a.offsets[g - 1];
+    const uint32_t end = a.radii[g] > 0 ? a.offsets[g] : start;
+    float s[NQ * 4];
+#pragma unroll
+    for (int i = 0; i < NQ * 4; ++i) s[i] = 0.f;
+    const int RS = a.RS;
+    for (uint32_t k = start; k < end; ++k) {
+        const float4* row = reinterpret_cast<const float4*>(a.rows + (size_t)k * RS);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (4 * q < RS) {
+                const float4 v = row[q];
+                s[4 * q] += v.x; s[4 * q + 1] += v.y; s[4 * q + 2] += v.z; s[4 * q + 3] += v.w;
+            }
+        }
+    }
+    a.dL_dmeans2D[3 * g + 0] = s[kRowMean + 0];
+    a.dL_dmeans2D[3 * g + 1] = s[kRowMean + 1];
+    a.dL_dmeans2D[3 * g + 2] = s[kRowMean + 2];
+    a.dL_dopacity[g] = s[kRowOpacity];
+    a.dL_dcolors[3 * g + 0] = s[kRowColor + 0];
+    a.dL_dcolors[3 * g + 1] = s[kRowColor + 1];
+    a.dL_dcolors[3 * g + 2] = s[kRowColor + 2];
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c)
+        if (c < a.S) a.dL_dfeatures[(size_t)g * a.S + c] = s[kRowFeat + c];
+
+    float* dmean3 = a.dL_dmeans3D + 3 * g;
+    float* dcov = a.dL_dcov3D + 6 * g;
+    if (!(a.radii[g] > 0)) {
+        dmean3[0] = dmean3[1] = dmean3[2] = 0.f;
+        for (int i = 0; i < 6; ++i) dcov[i] = 0.f;
+        if (a.dL_dsh)
+            for (int i = 0; i < 3 * a.M; ++i) a.dL_dsh[(size_t)g * a.M * 3 + i] = 0.f;
+        for (int i = 0; i < 3; ++i) a.dL_dscales[3 * g + i] = 0.f;
+        for (int i = 0; i < 4; ++i) a.dL_drotations[4 * g + i] = 0.f;
+        return;
+    }
+
+    // ---- computeCov2DCUDA (backward.cu:144-276) ----
+    const float h_x = a.focal_x, h_y = a.focal_y;
+    const float* view = a.view;
+    const float3 mean = make_float3(a.means3D[3 * g], a.means3D[3 * g + 1], a.means3D[3 * g + 2]);
+    const float* c3 = a.cov3D + 6 * g;
+    const float dcx = s[kRowConic + 0], dcy = s[kRowConic + 1], dcz = s[kRowConic + 2];
+    float3 t = xform_point4x3(mean, view);
+    const float limx = 1.3f * a.tan_fovx, limy = 1.3f * a.tan_fovy;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float x_grad_mul = txtz < -limx || txtz > limx ? 0.f : 1.f;
+    const float y_grad_mul = tytz < -limy || tytz > limy ? 0.f : 1.f;
+    const float j00 = h_x / t.z, j11 = h_y / t.z;
+    const float j20 = -(h_x * t.x) / (t.z * t.z), j21 = -(h_y * t.y) / (t.z * t.z);
+    float g0[3], g1[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        g0[r] = view[4 * r + 0] * j00 + view[4 * r + 2] * j20;
+        g1[r] = view[4 * r + 1] * j11 + view[4 * r + 2] * j21;
+    }
+    const float V[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
+    float u[3], vv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        u[k] = V[k][0] * g0[0] + V[k][1] * g0[1] + V[k][2] * g0[2];
+        vv[k] = V[k][0] * g1[0] + V[k][1] * g1[1] + V[k][2] * g1[2];
+    }
+    const float ca = g0[0] * u[0] + g0[1] * u[1] + g0[2] * u[2] + 0.3f;
+    const float cb = g1[0] * u[0] + g1[1] * u[1] + g1[2] * u[2];
+    const float cc = g1[0] * vv[0] + g1[1] * vv[1] + g1[2] * vv[2] + 0.3f;
+    const float denom = ca * cc - cb * cb;
+    float da = 0.f, db = 0.f, dc = 0.f;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    if (denom2inv != 0.f) {
+        da = denom2inv * (-cc * cc * dcx + 2 * cb * cc * dcy + (denom - ca * cc) * dcz);
+        dc = denom2inv * (-ca * ca * dcz + 2 * ca * cb * dcy + (denom - ca * cc) * dcx);
+        db = denom2inv * 2 * (cb * cc * dcx - (denom + 2 * cb * cb) * dcy + ca * cb * dcz);
+        dcov[0] = g0[0] * g0[0] * da + g0[0] * g1[0] * db + g1[0] * g1[0] * dc;
+        dcov[3] = g0[1] * g0[1] * da + g0[1] * g1[1] * db + g1[1] * g1[1] * dc;
+        dcov[5] = g0[2] * g0[2] * da + g0[2] * g1[2] * db + g1[2] * g1[2] * dc;
+        dcov[1] = 2 * g0[0] * g0[1] * da + (g0[0] * g1[1] + g0[1] * g1[0]) * db + 2 * g1[0] * g1[1] * dc;
+        dcov[2] = 2 * g0[0] * g0[2] * da + (g0[0] * g1[2] + g0[2] * g1[0]) * db + 2 * g1[0] * g1[2] * dc;
+        dcov[4] = 2 * g0[2] * g0[1] * da + (g0[1] * g1[2] + g0[2] * g1[1]) * db + 2 * g1[1] * g1[2] * dc;
+    } else {
+        for (int i = 0; i < 6; ++i) dcov[i] = 0.f;
+    }
+    float dT0[3], dT1[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float p0 = g0[0] * V[k][0] + g0[1] * V[k][1] + g0[2] * V[k][2];
+        const float p1 = g1[0] * V[k][0] + g1[1] * V[k][1] + g1[2] * V[k][2];
+        dT0[k] = 2 * p0 * da + p1 * db;
+        dT1[k] = 2 * p1 * dc + p0 * db;
+    }
+    const float dJ00 = view[0] * dT0[0] + view[4] * dT0[1] + view[8] * dT0[2];
+    const float dJ02 = view[2] * dT0[0] + view[6] * dT0[1] + view[10] * dT0[2];
+    const float dJ11 = view[1] * dT1[0] + view[5] * dT1[1] + view[9] * dT1[2];
+    const float dJ12 = view[2] * dT1[0] + view[6] * dT1[1] + view[10] * dT1[2];
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dtx = x_grad_mul * -h_x * tz2 * dJ02;
+    const float dty = y_grad_mul * -h_y * tz2 * dJ12;
+    const float dtz = -h_x * tz2 * dJ00 - h_y * tz2 * dJ11 + (2 * h_x * t.x) * tz3 * dJ02 + (2 * h_y * t.y) * tz3 * dJ12;
+    const float vz = dtz + s[kRowMean + 2];
+    float dm[3] = {view[0] * dtx + view[1] * dty + view[2] * vz, view[4] * dtx + view[5] * dty + view[6] * vz,
+                   view[8] * dtx + view[9] * dty + view[10] * vz};
+
+    // ---- preprocessCUDA backward (backward.cu:372-397) ----
+    const float* proj = a.proj;
+    const float4 mh = xform_point4x4(mean, proj);
+    const float m_w = 1.0f / (mh.w + 0.0000001f);
+    const float mul1 = (proj[0] * mean.x + proj[4] * mean.y + proj[8] * mean.z + proj[12]) * m_w * m_w;
+    const float mul2 = (proj[1] * mean.x + proj[5] * mean.y + proj[9] * mean.z + proj[13]) * m_w * m_w;
+    const float gx2 = s[kRowMean + 0], gy2 = s[kRowMean + 1];
+    dm[0] += (proj[0] * m_w - proj[3] * mul1) * gx2 + (proj[1] * m_w - proj[3] * mul2) * gy2;
+    dm[1] += (proj[4] * m_w - proj[7] * mul1) * gx2 + (proj[5] * m_w - proj[7] * mul2) * gy2;
+    dm[2] += (proj[8] * m_w - proj[11] * mul1) * gx2 + (proj[9] * m_w - proj[11] * mul2) * gy2;
+    if (a.sh) {
+        const uint8_t cl = a.clamped[g];
+        const float dRGB[3] = {s[kRowColor + 0] * ((cl & 1) ? 0.f : 1.f), s[kRowColor + 1] * ((cl & 2) ? 0.f : 1.f),
+                               s[kRowColor + 2] * ((cl & 4) ? 0.f : 1.f)};
+        sh_backward(a.D, a.M, mean, a.campos, a.sh + (size_t)g * a.M * 3, dRGB, dm, a.dL_dsh + (size_t)g * a.M * 3);
+    }
+    dmean3[0] = dm[0];
+    dmean3[1] = dm[1];
+    dmean3[2] = dm[2];
+    if (a.use_scales) {
+        const float3 sc = make_float3(a.scales[3 * g], a.scales[3 * g + 1], a.scales[3 * g + 2]);
+        const float4 q = make_float4(a.rotations[4 * g], a.rotations[4 * g + 1], a.rotations[4 * g + 2],
+                                     a.rotations[4 * g + 3]);
+        cov3d_backward(sc, a.scale_modifier, q, dcov, a.dL_dscales + 3 * g, a.dL_drotations + 4 * g);
+    } else {
+        for (int i = 0; i < 3; ++i) a.dL_dscales[3 * g + i] = 0.f;
+        for (int i = 0; i < 4; ++i) a.dL_drotations[4 * g + i] = 0.f;
+    }
+}
+
+template <int SMAX>
+static hipError_t launch_gather_s(const GatherBwdArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL((gather_bwd_kernel<SMAX>), dim3((a.P + 255) / 256), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_backward(const GatherBwdArgs& a, hipStream_t stream) {
+    if (a.P == 0) return hipSuccess;
+    if (a.S == 0) return launch_gather_s<0>(a, stream);
+    if (a.S <= 4) return launch_gather_s<4>(a, stream);
+    if (a.S <= 8) return launch_gather_s<8>(a, stream);
+    if (a.S <= 12) return launch_gather_s<12>(a, stream);
+    if (a.S <= 16) return launch_gather_s<16>(a, stream);
+    if (a.S <= 24) return launch_gather_s<24>(a, stream);
+    return launch_gather_s<32>(a, stream);
+}
+
+}  // namespace r3dg

@@ -1,0 +1,306 @@
+// render_fwd.hip -- front-to-back alpha blend per 16x16 screen tile (gfx950, wave64).
+//
+// Restates reference forward.cu:388-561 (renderCUDA) with an MI355X layout:
+//   * one 256-thread workgroup per tile; each wave64 owns an 8x8 quadrant (square, so the
+//     per-wave footprint test below rejects more Gaussians than 16x4 strips would);
+//   * each batch of 256 sorted instances is staged in LDS once: xy, conic|opacity, and an AoS
+//     attribute row (colour, depth, [shader colour], features) read with ds_read_b128
+//     broadcasts -- the reference re-reads colours and features from HBM per pixel;
+//   * a conservative per-quadrant footprint mask (alpha >= 1/255 ellipse, widened) lets a
+//     wave skip an instance with one scalar branch. Skipping is exact: a skipped instance
+//     would have failed the reference's alpha test on every pixel of the quadrant
+//     (tests/test_gpu_parity.py checks cull on == cull off bit for bit);
+//   * early exit per wave (ballot) and per block (__syncthreads_count), as the reference;
+//   * XCD-aware tile order (r3dg_kernels.h).
+#include "r3dg_common.h"
+#include "r3dg_kernels.h"
+
+namespace r3dg {
+
+// Conservative set of 8x8 quadrants of tile (x0,y0) in which alpha = o*exp(power) can reach
+// 1/255. power = -Q/2 with Q = a dx^2 + 2b dx dy + c dy^2; alpha >= 1/255 needs
+// Q <= t = 2 ln(255 o). The ellipse Q <= t has half extents sqrt(t * cov_xx), sqrt(t * cov_yy)
+// with cov = conic^-1. Widened by 10 % + 0.1 in t and 1 px in extent to cover fp32 rounding
+// of power and __expf.
+__device__ __forceinline__ uint32_t quadrant_mask(float2 xy, float4 co, int x0, int y0, int cull) {
+    if (!cull) return 0xFu;
+    if (co.w < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 everywhere
+    const float det = co.x * co.z - co.y * co.y;
+    if (!(det > 0.0f)) return 0xFu;
+    const float t = 2.0f * __logf(255.0f * co.w) * 1.1f + 0.1f;
+    const float ex = sqrtf(t * co.z / det) + 1.0f;
+    const float ey = sqrtf(t * co.x / det) + 1.0f;
+    if (!(ex < 1e30f) || !(ey < 1e30f)) return 0xFu;
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float qx = (float)(x0 + (q & 1) * 8), qy = (float)(y0 + (q >> 1) * 8);
+        if (xy.x + ex >= qx && xy.x - ex <= qx + 7.0f && xy.y + ey >= qy && xy.y - ey <= qy + 7.0f) m |= 1u << q;
+    }
+    return m;
+}
+
+template <int SMAX, bool SHADER>
+__global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
+    constexpr int FO = SHADER ? 8 : 4;                 // feature offset inside the attribute row
+    constexpr int NA4 = (FO + SMAX + 3) / 4;           // float4 per attribute row
+    __shared__ float2 s_xy[kBlock];
+    __shared__ float4 s_co[kBlock];
+    __shared__ uint32_t s_mask[kBlock];
+    __shared__ float4 s_attr[kBlock * NA4];
+
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (tile >= a.num_tiles) return;
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
+    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const float pfx = (float)px, pfy = (float)py;
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+
+    bool done = !inside;
+    float T = 1.0f;
+    uint32_t last = 0;
+    float C[3] = {0.f, 0.f, 0.f}, CS[3] = {0.f, 0.f, 0.f}, F[SMAX > 0 ? SMAX : 1];
+    float Dp = 0.f, Op = 0.f;
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c) F[c] = 0.f;
+
+    for (int base = 0; base < n; base += kBlock) {
+        if (__syncthreads_count(done) == kBlock) break;
+        if (base + t < n) {
+            const uint32_t gid = a.point_list[range.x + base + t];
+            const float2 xy = a.means2D[gid];
+            const float4 co = a.conic_opacity[gid];
+            s_xy[t] = xy;
+            s_co[t] = co;
+            s_mask[t] = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
+            float v[NA4 * 4];
+#pragma unroll
+            for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
+            v[0] = a.colors[3 * gid + 0];
+            v[1] = a.colors[3 * gid + 1];
+            v[2] = a.colors[3 * gid + 2];
+            v[3] = a.depths[gid];
+            if constexpr (SHADER) {
+                v[4] = a.shader_colors[3 * gid + 0];
+                v[5] = a.shader_colors[3 * gid + 1];
+                v[6] = a.shader_colors[3 * gid + 2];
+            }
+            const float* f = a.features + (size_t)gid * a.S;
+#pragma unroll
+            for (int c = 0; c < SMAX; ++c)
+                if (c < a.S) v[FO + c] = f[c];
+#pragma unroll
+            for (int q = 0; q < NA4; ++q)
+                s_attr[t * NA4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        }
+        __syncthreads();
+        const int cnt = min(kBlock, n - base);
+        if (__ballot(!done) != 0ull) {
+            for (int j = 0; j < cnt; ++j) {
+                const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
+                if (!((m >> w) & 1u)) continue;
+                if (!done) {
+                    const float2 xy = s_xy[j];
+                    const float4 co = s_co[j];
+                    const float dx = xy.x - pfx, dy = xy.y - pfy;
+                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    if (!(power > 0.0f)) {
+                        const float alpha = fminf(0.99f, co.w * __expf(power));
+                        if (!(alpha < 1.0f / 255.0f)) {
+                            const float test_T = T * (1.0f - alpha);
+                            if (test_T < 0.0001f) {
+                                done = true;
+                            } else {
+                                const float wgt = alpha * T;
+                                float v[NA4 * 4];
+#pragma unroll
+                                for (int q = 0; q < NA4; ++q) {
+                                    const float4 r = s_attr[j * NA4 + q];
+                                    v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
+                                }
+                                C[0] += v[0] * wgt;
+                                C[1] += v[1] * wgt;
+                                C[2] += v[2] * wgt;
+                                if constexpr (SHADER) {
+                                    CS[0] += v[4] * wgt;
+                                    CS[1] += v[5] * wgt;
+                                    CS[2] += v[6] * wgt;
+                                }
+#pragma unroll
+                                for (int c = 0; c < SMAX; ++c) F[c] += v[FO + c] * wgt;
+                                Dp += v[3] * wgt;
+                                Op += wgt;
+                                T = test_T;
+                                last = (uint32_t)(base + j + 1);
+                            }
+                        }
+                    }
+                }
+                if (__ballot(!done) == 0ull) break;
+            }
+        }
+    }
+
+    if (inside) {
+        const int pix = py * a.W + px;
+        a.final_T[pix] = T;
+        a.n_contrib[pix] = last;
+        const float b0 = a.bg[0], b1 = a.bg[1], b2 = a.bg[2];
+        a.out_color[3 * pix + 0] = C[0] + T * b0;
+        a.out_color[3 * pix + 1] = C[1] + T * b1;
+        a.out_color[3 * pix + 2] = C[2] + T * b2;
+        if constexpr (SHADER) {
+            a.out_shader_color[3 * pix + 0] = CS[0] + T * b0;
+            a.out_shader_color[3 * pix + 1] = CS[1] + T * b1;
+            a.out_shader_color[3 * pix + 2] = CS[2] + T * b2;
+        } else {
+            // default splat shader: shader colour == SH colour (splatShader.cu:67-71)
+            a.out_shader_color[3 * pix + 0] = C[0] + T * b0;
+            a.out_shader_color[3 * pix + 1] = C[1] + T * b1;
+            a.out_shader_color[3 * pix + 2] = C[2] + T * b2;
+        }
+        a.out_depth[pix] = Dp;
+        a.out_opacity[pix] = Op;
+#pragma unroll
+        for (int c = 0; c < SMAX; ++c)
+            if (c < a.S) a.out_feature[a.flay.a[c] + pix * a.flay.m[c]] = F[c];
+    }
+}
+
+template <int SMAX>
+static hipError_t launch_fwd_s(const RenderFwdArgs& a, bool shader, hipStream_t stream) {
+    const int grid = padded_tile_grid(a.num_tiles);
+    if (shader)
+        hipLaunchKernelGGL((render_fwd_kernel<SMAX, true>), dim3(grid), dim3(kBlock), 0, stream, a);
+    else
+        hipLaunchKernelGGL((render_fwd_kernel<SMAX, false>), dim3(grid), dim3(kBlock), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_render_forward(const RenderFwdArgs& a, bool shader, hipStream_t stream) {
+    if (a.num_tiles == 0) return hipSuccess;
+    if (a.S == 0) return launch_fwd_s<0>(a, shader, stream);
+    if (a.S <= 4) return launch_fwd_s<4>(a, shader, stream);
+    if (a.S <= 8) return launch_fwd_s<8>(a, shader, stream);
+    if (a.S <= 12) return launch_fwd_s<12>(a, shader, stream);
+    if (a.S <= 16) return launch_fwd_s<16>(a, shader, stream);
+    if (a.S <= 24) return launch_fwd_s<24>(a, shader, stream);
+    return launch_fwd_s<32>(a, shader, stream);
+}
+
+// forward.cu:271-383 (RenderIntermediateTexturesCUDA): depth and stencil blend for the splat
+// shaders. Only launched when a non-default splat shader is active; the Stencil accumulator
+// starts at 0 (the reference leaves it uninitialised, forward.cu:312).
+__global__ void __launch_bounds__(kBlock) intermediate_kernel(IntermediateArgs a) {
+    __shared__ float2 s_xy[kBlock];
+    __shared__ float4 s_co[kBlock];
+    __shared__ float2 s_ds[kBlock];  // depth, stencil value
+    __shared__ float s_so[kBlock];
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (tile >= a.num_tiles) return;
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
+    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+    bool done = !inside;
+    float sT = 1.f, T = 1.f, St = 0.f, Dp = 0.f;
+    for (int base = 0; base < n; base += kBlock) {
+        if (__syncthreads_count(done) == kBlock) break;
+        if (base + t < n) {
+            const uint32_t gid = a.point_list[range.x + base + t];
+            s_xy[t] = a.means2D[gid];
+            s_co[t] = a.conic_opacity[gid];
+            s_ds[t] = make_float2(a.depths[gid], a.stencils[gid]);
+            s_so[t] = a.stencil_opacity[gid];
+        }
+        __syncthreads();
+        const int cnt = min(kBlock, n - base);
+        for (int j = 0; !done && j < cnt; ++j) {
+            const float2 xy = s_xy[j];
+            const float4 co = s_co[j];
+            const float dx = xy.x - (float)px, dy = xy.y - (float)py;
+            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            if (power > 0.0f) continue;
+            const float G = __expf(power);
+            const float alpha = fminf(0.99f, co.w * G);
+            const float salpha = fminf(0.99f, s_so[j] * G);
+            if (alpha < 1.0f / 255.0f && salpha < 1.0f / 255.0f) continue;
+            const float tT = T * (1 - alpha), tS = sT * (1 - salpha);
+            if (tT < 0.0001f && tS < 0.0001f) {
+                done = true;
+                continue;
+            }
+            Dp += s_ds[j].x * (alpha * T);
+            T = tT;
+            St += s_ds[j].y * (salpha * sT);
+            sT = tS;
+        }
+    }
+    if (inside) {
+        const int pix = py * a.W + px;
+        a.out_depth[pix] = Dp;
+        a.out_stencil[pix] = St;
+    }
+}
+
+// forward.cu:564-658 (renderSurfaceXYZCUDA + renderPseudoNormalCUDA) fused: every thread
+// recomputes its 3x3 neighbourhood's surface points from depth/opacity (same expression as
+// the xyz it stores), so one pass produces both outputs.
+__device__ __forceinline__ float3 surface_point(const XyzNormalArgs& a, int x, int y) {
+    const int pix = y * a.W + x;
+    const float d = a.depth[pix] / fmaxf(a.opacity[pix], 0.0000001f);
+    return make_float3(((float)x - a.cx) / a.focal_x * d, ((float)y - a.cy) / a.focal_y * d, d);
+}
+
+__global__ void __launch_bounds__(256) xyz_normal_kernel(XyzNormalArgs a) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.W || y >= a.H) return;
+    const int pix = y * a.W + x;
+    const int ym = y == 0 ? 0 : y - 1, yp = y == a.H - 1 ? a.H - 1 : y + 1;
+    const int xm = x == 0 ? 0 : x - 1, xp = x == a.W - 1 ? a.W - 1 : x + 1;
+    const float3 c = surface_point(a, x, y);
+    a.xyz[3 * pix + 0] = c.x;
+    a.xyz[3 * pix + 1] = c.y;
+    a.xyz[3 * pix + 2] = c.z;
+    const float3 p00 = surface_point(a, xm, ym), p01 = surface_point(a, x, ym), p02 = surface_point(a, xp, ym);
+    const float3 p10 = surface_point(a, xm, y), p12 = surface_point(a, xp, y);
+    const float3 p20 = surface_point(a, xm, yp), p21 = surface_point(a, x, yp), p22 = surface_point(a, xp, yp);
+    float ga[3], gb[3];
+    const float3 q00 = p00, q01 = p01, q02 = p02, q10 = p10, q12 = p12, q20 = p20, q21 = p21, q22 = p22;
+    const float* f00 = &q00.x; const float* f01 = &q01.x; const float* f02 = &q02.x; const float* f10 = &q10.x;
+    const float* f12 = &q12.x; const float* f20 = &q20.x; const float* f21 = &q21.x; const float* f22 = &q22.x;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        ga[i] = -0.125f * f00[i] + 0.125f * f02[i] - 0.25f * f10[i] + 0.25f * f12[i] - 0.125f * f20[i] +
+                0.125f * f22[i];
+        gb[i] = -0.125f * f00[i] - 0.25f * f01[i] - 0.125f * f02[i] + 0.125f * f20[i] + 0.25f * f21[i] +
+                0.125f * f22[i];
+    }
+    float nx = ga[1] * gb[2] - ga[2] * gb[1];
+    float ny = -ga[0] * gb[2] + ga[2] * gb[0];
+    float nz = ga[0] * gb[1] - ga[1] * gb[0];
+    const float norm = sqrtf(nx * nx + ny * ny + nz * nz);
+    if (norm <= 0.0f) {
+        a.normal[3 * pix + 0] = 0.f;
+        a.normal[3 * pix + 1] = 0.f;
+        a.normal[3 * pix + 2] = 0.f;
+        return;
+    }
+    nx = -nx / norm;
+    ny = -ny / norm;
+    nz = -nz / norm;
+    const float* v = a.view;
+    a.normal[3 * pix + 0] = v[0] * nx + v[1] * ny + v[2] * nz;
+    a.normal[3 * pix + 1] = v[4] * nx + v[5] * ny + v[6] * nz;
+    a.normal[3 * pix + 2] = v[8] * nx + v[9] * ny + v[10] * nz;
+}
+
+}  // namespace r3dg

@@ -1,0 +1,490 @@
+// torch_ext.cpp -- pybind module `_C`: the reference operator surface over the C ABI.
+//
+// Mirrors r3dg_rasterization._C (reference r3dg-rasterization/ext.cu:21-35): the same 14
+// function names, argument order and return tuples, so gaussian_renderer/neilf.py and
+// scene/gaussian_model.py call it unchanged. Documented extensions:
+//   (1) None / 0 shader-manager, texture and post-pass handles mean "defaults";
+//   (2) every launch goes on the current HIP stream of means3D's device, and all buffers
+//       (including the three state buffers) live on that device;
+//   (3) extra entry points used by the shipped wrapper and the parity tests
+//       (rasterize_gaussians_backward_ex, render_equation_forward_with_rand, rasterizer_state,
+//       feature_groups, create_shader_manager, shader_manager_info).
+// Errors from the C ABI surface as RuntimeError with the library's message.
+#include <torch/extension.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include <map>
+#include <optional>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "r3dg_hip.h"
+
+namespace {
+
+void check(int rc, const char* what) {
+    if (rc != R3DG_OK) throw std::runtime_error(std::string(what) + ": " + r3dg_last_error());
+}
+
+// empty tensor (numel 0) means "absent", as the reference's data_ptr of an empty tensor
+const float* opt_ptr(const torch::Tensor& t) { return t.numel() == 0 ? nullptr : t.data_ptr<float>(); }
+
+torch::Tensor dev_contig(const torch::Tensor& t, const torch::Device& dev) {
+    if (t.numel() == 0) return t;
+    TORCH_CHECK(t.scalar_type() == torch::kFloat32, "expected a float32 tensor");
+    return t.to(dev).contiguous();
+}
+
+struct TensorAlloc {
+    torch::TensorOptions opts;
+    torch::Tensor t;
+};
+void* tensor_alloc(void* ctx, size_t n) {
+    auto* a = static_cast<TensorAlloc*>(ctx);
+    a->t = torch::empty({(int64_t)std::max<size_t>(n, 256)}, a->opts);
+    return a->t.data_ptr();
+}
+
+r3dg_stream_t stream_of(const torch::Device& dev) {
+    return (r3dg_stream_t)c10::hip::getCurrentHIPStream(dev.index()).stream();
+}
+
+using FwdResult = std::tuple<int, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor,
+                             torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor,
+                             torch::Tensor, torch::Tensor, torch::Tensor>;
+
+// RasterizeGaussiansCUDA (rasterize_points.cu:39-181)
+FwdResult rasterize_gaussians(const torch::Tensor& background, double time, double dt, const torch::Tensor& means3D,
+                              const torch::Tensor& features, const torch::Tensor& colors,
+                              const torch::Tensor& opacity, const torch::Tensor& scales,
+                              const torch::Tensor& rotations, double scale_modifier,
+                              const torch::Tensor& cov3D_precomp, const torch::Tensor& viewmatrix,
+                              const torch::Tensor& viewmatrix_inv, const torch::Tensor& projmatrix,
+                              const torch::Tensor& projmatrix_inv, double tan_fovx, double tan_fovy, double cx,
+                              double cy, int64_t image_height, int64_t image_width, const torch::Tensor& sh,
+                              int64_t degree, const torch::Tensor& campos, bool prefiltered,
+                              bool computer_pseudo_normal, std::optional<int64_t> d_textureManager_ptr,
+                              std::optional<int64_t> h_shShaderManager_ptr,
+                              std::optional<int64_t> h_splatShaderManager_ptr,
+                              std::optional<std::vector<int64_t>> postProcessingPasses, bool debug) {
+    if (means3D.ndimension() != 2 || means3D.size(1) != 3)
+        throw std::runtime_error("means3D must have dimensions (num_points, 3)");
+    TORCH_CHECK(means3D.is_cuda(), "means3D must be a GPU tensor (this build has no CPU path)");
+    const torch::Device dev = means3D.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    const int P = (int)means3D.size(0);
+    const int S = features.numel() == 0 && features.dim() < 2 ? 0 : (int)features.size(1);
+    const int H = (int)image_height, W = (int)image_width;
+    auto fopt = means3D.options().dtype(torch::kFloat32);
+
+    auto m3 = dev_contig(means3D, dev), ft = dev_contig(features, dev), co = dev_contig(colors, dev);
+    auto op = dev_contig(opacity, dev), sc = dev_contig(scales, dev), ro = dev_contig(rotations, dev);
+    auto c3 = dev_contig(cov3D_precomp, dev), shc = dev_contig(sh, dev), bg = dev_contig(background, dev);
+    auto vm = dev_contig(viewmatrix, dev), vmi = dev_contig(viewmatrix_inv, dev);
+    auto pm = dev_contig(projmatrix, dev), pmi = dev_contig(projmatrix_inv, dev), cp = dev_contig(campos, dev);
+
+    torch::Tensor out_color = torch::empty({H, W, 3}, fopt);
+    torch::Tensor out_opacity = torch::empty({H, W, 1}, fopt);
+    torch::Tensor out_depth = torch::empty({H, W, 1}, fopt);
+    torch::Tensor out_stencil = torch::empty({H, W, 1}, fopt);
+    torch::Tensor out_feature = torch::empty({H, W, S}, fopt);
+    torch::Tensor out_shader = torch::empty({H, W, 3}, fopt);
+    torch::Tensor out_normal = torch::empty({H, W, 3}, fopt);
+    torch::Tensor out_xyz = torch::empty({H, W, 3}, fopt);
+    torch::Tensor radii = torch::empty({P}, means3D.options().dtype(torch::kInt32));
+
+    auto bopt = torch::TensorOptions().dtype(torch::kUInt8).device(dev);
+    TensorAlloc ga{bopt, torch::empty({0}, bopt)}, ba{bopt, torch::empty({0}, bopt)}, ia{bopt, torch::empty({0}, bopt)};
+
+    std::vector<int64_t> passes = postProcessingPasses.value_or(std::vector<int64_t>{});
+    r3dg_raster_settings s{};
+    s.P = P; s.S = S; s.D = (int)degree; s.M = shc.numel() == 0 ? 0 : (int)shc.size(1);
+    s.W = W; s.H = H;
+    s.tan_fovx = (float)tan_fovx; s.tan_fovy = (float)tan_fovy; s.cx = (float)cx; s.cy = (float)cy;
+    s.scale_modifier = (float)scale_modifier; s.time = (float)time; s.dt = (float)dt;
+    s.prefiltered = prefiltered; s.compute_pseudo_normal = computer_pseudo_normal; s.debug = debug;
+    s.bg = bg.data_ptr<float>();
+    s.viewmatrix = vm.data_ptr<float>(); s.viewmatrix_inv = opt_ptr(vmi);
+    s.projmatrix = pm.data_ptr<float>(); s.projmatrix_inv = opt_ptr(pmi);
+    s.campos = cp.data_ptr<float>();
+    s.sh_shader_manager = h_shShaderManager_ptr.value_or(0);
+    s.splat_shader_manager = h_splatShaderManager_ptr.value_or(0);
+    s.texture_manager = d_textureManager_ptr.value_or(0);
+    s.post_passes = passes.data();
+    s.n_post_passes = (int)passes.size();
+    r3dg_gaussians g{};
+    g.means3D = m3.data_ptr<float>(); g.features = opt_ptr(ft); g.colors_precomp = opt_ptr(co);
+    g.opacity = opt_ptr(op); g.scales = opt_ptr(sc); g.rotations = opt_ptr(ro);
+    g.cov3D_precomp = opt_ptr(c3); g.sh = opt_ptr(shc);
+    r3dg_forward_outputs o{};
+    o.color = out_color.data_ptr<float>(); o.opacity = out_opacity.data_ptr<float>();
+    o.depth = out_depth.data_ptr<float>(); o.stencil = out_stencil.data_ptr<float>();
+    o.feature = S > 0 ? out_feature.data_ptr<float>() : nullptr; o.shader_color = out_shader.data_ptr<float>();
+    o.normal = out_normal.data_ptr<float>(); o.surface_xyz = out_xyz.data_ptr<float>();
+    o.radii = P > 0 ? radii.data_ptr<int>() : nullptr;
+    int rendered = 0;
+    check(r3dg_rasterize_gaussians(&s, &g, &o, tensor_alloc, &ga, tensor_alloc, &ba, tensor_alloc, &ia, &rendered,
+                                   stream_of(dev)),
+          "rasterize_gaussians");
+    // n_contrib is a view into the image state buffer (reference: from_blob, rasterize_points.cu:179)
+    const int64_t off = (int64_t)r3dg_image_state_n_contrib_offset(H, W);
+    torch::Tensor n_contrib = ia.t.narrow(0, off, (int64_t)H * W * 4).view(torch::kInt32).view({H, W, 1});
+    return {rendered, n_contrib, out_color, out_opacity, out_depth, out_stencil, out_feature, out_shader,
+            out_normal, out_xyz, radii, ga.t, ba.t, ia.t};
+}
+
+using BwdResult = std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor,
+                             torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor>;
+
+BwdResult backward_impl(const torch::Tensor& background, const torch::Tensor& means3D, const torch::Tensor& features,
+                        const torch::Tensor& radii, const torch::Tensor& colors, const torch::Tensor& scales,
+                        const torch::Tensor& rotations, double scale_modifier, const torch::Tensor& cov3D_precomp,
+                        const torch::Tensor& viewmatrix, const torch::Tensor& projmatrix, double tan_fovx,
+                        double tan_fovy, const torch::Tensor& dL_dout_color, const torch::Tensor& dL_dout_opacity,
+                        const torch::Tensor& dL_dout_depth, const torch::Tensor& dL_dout_feature,
+                        const torch::Tensor& sh, int64_t degree, const torch::Tensor& campos,
+                        const torch::Tensor& geomBuffer, int64_t R, const torch::Tensor& binningBuffer,
+                        const torch::Tensor& imageBuffer, bool backward_geometry, bool debug, int H, int W,
+                        bool color_hwc, bool feature_native) {
+    const torch::Device dev = means3D.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    const int P = (int)means3D.size(0);
+    const int S = features.numel() == 0 && features.dim() < 2 ? 0 : (int)features.size(1);
+    const int M = sh.numel() == 0 ? 0 : (int)sh.size(1);
+    auto fopt = means3D.options().dtype(torch::kFloat32);
+    torch::Tensor dL_dmeans3D = torch::empty({P, 3}, fopt);
+    torch::Tensor dL_dmeans2D = torch::empty({P, 3}, fopt);
+    torch::Tensor dL_dfeatures = torch::empty({P, S}, fopt);
+    torch::Tensor dL_dcolors = torch::empty({P, 3}, fopt);
+    torch::Tensor dL_dopacity = torch::empty({P, 1}, fopt);
+    torch::Tensor dL_dcov3D = torch::empty({P, 6}, fopt);
+    torch::Tensor dL_dsh = torch::empty({P, M, 3}, fopt);
+    torch::Tensor dL_dscales = torch::empty({P, 3}, fopt);
+    torch::Tensor dL_drotations = torch::empty({P, 4}, fopt);
+    if (P == 0) return {dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dfeatures, dL_dcov3D, dL_dsh,
+                        dL_dscales, dL_drotations};
+
+    auto m3 = dev_contig(means3D, dev), ft = dev_contig(features, dev), co = dev_contig(colors, dev);
+    auto sc = dev_contig(scales, dev), ro = dev_contig(rotations, dev), c3 = dev_contig(cov3D_precomp, dev);
+    auto shc = dev_contig(sh, dev), bg = dev_contig(background, dev), vm = dev_contig(viewmatrix, dev);
+    auto pm = dev_contig(projmatrix, dev), cp = dev_contig(campos, dev);
+    auto gc = dev_contig(dL_dout_color, dev), go = dev_contig(dL_dout_opacity, dev);
+    auto gd = dev_contig(dL_dout_depth, dev), gf = dev_contig(dL_dout_feature, dev);
+    torch::Tensor rad = radii.to(dev).to(torch::kInt32).contiguous();
+
+    r3dg_raster_settings s{};
+    s.P = P; s.S = S; s.D = (int)degree; s.M = M; s.W = W; s.H = H;
+    s.tan_fovx = (float)tan_fovx; s.tan_fovy = (float)tan_fovy; s.scale_modifier = (float)scale_modifier;
+    s.debug = debug;
+    s.bg = bg.data_ptr<float>(); s.viewmatrix = vm.data_ptr<float>(); s.projmatrix = pm.data_ptr<float>();
+    s.campos = cp.data_ptr<float>();
+    r3dg_gaussians g{};
+    g.means3D = m3.data_ptr<float>(); g.features = opt_ptr(ft); g.colors_precomp = opt_ptr(co);
+    g.scales = opt_ptr(sc); g.rotations = opt_ptr(ro); g.cov3D_precomp = opt_ptr(c3); g.sh = opt_ptr(shc);
+    r3dg_backward_grads gr{};
+    gr.dL_dout_color = gc.data_ptr<float>(); gr.color_hwc = color_hwc;
+    gr.dL_dout_opacity = go.data_ptr<float>(); gr.dL_dout_depth = gd.data_ptr<float>();
+    gr.dL_dout_feature = S > 0 ? gf.data_ptr<float>() : nullptr; gr.feature_native = feature_native;
+    r3dg_backward_outputs o{};
+    o.dL_dmeans2D = dL_dmeans2D.data_ptr<float>(); o.dL_dcolors = dL_dcolors.data_ptr<float>();
+    o.dL_dopacity = dL_dopacity.data_ptr<float>(); o.dL_dmeans3D = dL_dmeans3D.data_ptr<float>();
+    o.dL_dfeatures = S > 0 ? dL_dfeatures.data_ptr<float>() : nullptr; o.dL_dcov3D = dL_dcov3D.data_ptr<float>();
+    o.dL_dsh = M > 0 ? dL_dsh.data_ptr<float>() : nullptr; o.dL_dscales = dL_dscales.data_ptr<float>();
+    o.dL_drotations = dL_drotations.data_ptr<float>();
+    auto bopt = torch::TensorOptions().dtype(torch::kUInt8).device(dev);
+    TensorAlloc scratch{bopt, torch::empty({0}, bopt)};
+    check(r3dg_rasterize_gaussians_backward(&s, &g, rad.data_ptr<int>(), &gr, geomBuffer.data_ptr(),
+                                            binningBuffer.data_ptr(), imageBuffer.data_ptr(), (int)R,
+                                            backward_geometry, tensor_alloc, &scratch, &o, stream_of(dev)),
+          "rasterize_gaussians_backward");
+    return {dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dfeatures, dL_dcov3D, dL_dsh, dL_dscales,
+            dL_drotations};
+}
+
+// RasterizeGaussiansBackwardCUDA (rasterize_points.cu:183-275): grads are CHW / planar.
+BwdResult rasterize_gaussians_backward(const torch::Tensor& background, const torch::Tensor& means3D,
+                                       const torch::Tensor& features, const torch::Tensor& radii,
+                                       const torch::Tensor& colors, const torch::Tensor& scales,
+                                       const torch::Tensor& rotations, double scale_modifier,
+                                       const torch::Tensor& cov3D_precomp, const torch::Tensor& viewmatrix,
+                                       const torch::Tensor& projmatrix, double tan_fovx, double tan_fovy,
+                                       const torch::Tensor& dL_dout_color, const torch::Tensor& dL_dout_opacity,
+                                       const torch::Tensor& dL_dout_depth, const torch::Tensor& dL_dout_feature,
+                                       const torch::Tensor& sh, int64_t degree, const torch::Tensor& campos,
+                                       const torch::Tensor& geomBuffer, int64_t R, const torch::Tensor& binningBuffer,
+                                       const torch::Tensor& imageBuffer, bool backward_geometry, bool debug) {
+    const int H = (int)dL_dout_color.size(1), W = (int)dL_dout_color.size(2);
+    return backward_impl(background, means3D, features, radii, colors, scales, rotations, scale_modifier,
+                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_opacity,
+                         dL_dout_depth, dL_dout_feature, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                         backward_geometry, debug, H, W, false, false);
+}
+
+// Same, taking the forward's own output layouts (HWC colour, native feature layout): the
+// shipped autograd wrapper uses this so no transposes are needed.
+BwdResult rasterize_gaussians_backward_ex(const torch::Tensor& background, const torch::Tensor& means3D,
+                                          const torch::Tensor& features, const torch::Tensor& radii,
+                                          const torch::Tensor& colors, const torch::Tensor& scales,
+                                          const torch::Tensor& rotations, double scale_modifier,
+                                          const torch::Tensor& cov3D_precomp, const torch::Tensor& viewmatrix,
+                                          const torch::Tensor& projmatrix, double tan_fovx, double tan_fovy,
+                                          const torch::Tensor& dL_dout_color, const torch::Tensor& dL_dout_opacity,
+                                          const torch::Tensor& dL_dout_depth, const torch::Tensor& dL_dout_feature,
+                                          const torch::Tensor& sh, int64_t degree, const torch::Tensor& campos,
+                                          const torch::Tensor& geomBuffer, int64_t R,
+                                          const torch::Tensor& binningBuffer, const torch::Tensor& imageBuffer,
+                                          bool backward_geometry, bool debug, int64_t H, int64_t W) {
+    return backward_impl(background, means3D, features, radii, colors, scales, rotations, scale_modifier,
+                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_opacity,
+                         dL_dout_depth, dL_dout_feature, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                         backward_geometry, debug, (int)H, (int)W, true, true);
+}
+
+torch::Tensor mark_visible(torch::Tensor& means3D, torch::Tensor& viewmatrix, torch::Tensor& projmatrix) {
+    const torch::Device dev = means3D.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    const int P = (int)means3D.size(0);
+    torch::Tensor present = torch::zeros({P}, means3D.options().dtype(torch::kBool));
+    if (P == 0) return present;
+    auto m3 = dev_contig(means3D, dev), vm = dev_contig(viewmatrix, dev), pm = dev_contig(projmatrix, dev);
+    check(r3dg_mark_visible(P, m3.data_ptr<float>(), vm.data_ptr<float>(), pm.data_ptr<float>(),
+                            (uint8_t*)present.data_ptr<bool>(), stream_of(dev)),
+          "mark_visible");
+    return present;
+}
+
+r3dg_brdf_inputs brdf_inputs(const std::vector<torch::Tensor>& t, int sample_num) {
+    r3dg_brdf_inputs in{};
+    in.P = (int)t[0].size(0);
+    in.S_incident = (int)t[5].size(1);
+    in.S_direct = (int)t[6].size(1);
+    in.S_visibility = (int)t[7].size(1);
+    in.sample_num = sample_num;
+    in.base_color = t[0].data_ptr<float>(); in.roughness = t[1].data_ptr<float>();
+    in.metallic = t[2].data_ptr<float>(); in.normals = t[3].data_ptr<float>();
+    in.viewdirs = t[4].data_ptr<float>(); in.incidents_shs = t[5].data_ptr<float>();
+    in.direct_shs = t[6].data_ptr<float>(); in.visibility_shs = t[7].data_ptr<float>();
+    return in;
+}
+
+std::vector<torch::Tensor> prep_brdf(std::initializer_list<torch::Tensor> ts, const torch::Device& dev) {
+    std::vector<torch::Tensor> r;
+    for (const auto& t : ts) {
+        TORCH_CHECK(t.scalar_type() == torch::kFloat32, "render_equation: expected float32 inputs");
+        r.push_back(t.to(dev).contiguous());
+    }
+    return r;
+}
+
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> render_equation_forward_impl(
+    const std::vector<torch::Tensor>& t, int64_t sample_num, bool is_training, const torch::Tensor* rand_in) {
+    const torch::Device dev = t[0].device();
+    const int P = (int)t[0].size(0);
+    auto fopt = t[0].options().dtype(torch::kFloat32);
+    torch::Tensor pbr = torch::empty({P, 3}, fopt);
+    torch::Tensor dirs = torch::empty({P, sample_num, 3}, fopt);
+    torch::Tensor diffuse = torch::empty({P, 3}, fopt);
+    // the reference always draws the per-(Gaussian, sample) rotation (render_equation.cu:708)
+    torch::Tensor rnd = rand_in ? rand_in->to(dev).contiguous() : torch::rand({P, sample_num, 1}, fopt);
+    r3dg_brdf_inputs in = brdf_inputs(t, (int)sample_num);
+    check(r3dg_render_equation_forward(&in, is_training, rnd.numel() ? rnd.data_ptr<float>() : nullptr,
+                                       pbr.data_ptr<float>(), dirs.data_ptr<float>(), diffuse.data_ptr<float>(),
+                                       stream_of(dev)),
+          "render_equation_forward");
+    return {pbr, dirs, diffuse};
+}
+
+// RenderEquationForwardCUDA (render_equation.cu:688-726)
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> render_equation_forward(
+    const torch::Tensor& base_color, const torch::Tensor& roughness, const torch::Tensor& metallic,
+    const torch::Tensor& normals, const torch::Tensor& viewdirs, const torch::Tensor& incidents_shs,
+    const torch::Tensor& direct_shs, const torch::Tensor& visibility_shs, int64_t sample_num, bool is_training,
+    bool debug) {
+    (void)debug;
+    const torch::Device dev = base_color.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    auto t = prep_brdf({base_color, roughness, metallic, normals, viewdirs, incidents_shs, direct_shs, visibility_shs},
+                       dev);
+    return render_equation_forward_impl(t, sample_num, is_training, nullptr);
+}
+
+// test entry: explicit rotation randoms [P, sample_num(, 1)]
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> render_equation_forward_with_rand(
+    const torch::Tensor& base_color, const torch::Tensor& roughness, const torch::Tensor& metallic,
+    const torch::Tensor& normals, const torch::Tensor& viewdirs, const torch::Tensor& incidents_shs,
+    const torch::Tensor& direct_shs, const torch::Tensor& visibility_shs, int64_t sample_num, bool is_training,
+    const torch::Tensor& rand_float) {
+    const torch::Device dev = base_color.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    auto t = prep_brdf({base_color, roughness, metallic, normals, viewdirs, incidents_shs, direct_shs, visibility_shs},
+                       dev);
+    return render_equation_forward_impl(t, sample_num, is_training, &rand_float);
+}
+
+// RenderEquationForwardCUDA_complex (render_equation.cu:220-274)
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor,
+           torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor>
+render_equation_forward_complex(const torch::Tensor& base_color, const torch::Tensor& roughness,
+                                const torch::Tensor& metallic, const torch::Tensor& normals,
+                                const torch::Tensor& viewdirs, const torch::Tensor& incidents_shs,
+                                const torch::Tensor& direct_shs, const torch::Tensor& visibility_shs,
+                                int64_t sample_num) {
+    const torch::Device dev = base_color.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    auto t = prep_brdf({base_color, roughness, metallic, normals, viewdirs, incidents_shs, direct_shs, visibility_shs},
+                       dev);
+    const int P = (int)t[0].size(0);
+    const int64_t Ns = sample_num;
+    auto fopt = t[0].options().dtype(torch::kFloat32);
+    torch::Tensor pbr = torch::empty({P, 3}, fopt), dirs = torch::empty({P, Ns, 3}, fopt);
+    torch::Tensor lights = torch::empty({P, Ns, 3}, fopt), local = torch::empty({P, Ns, 3}, fopt);
+    torch::Tensor global = torch::empty({P, Ns, 3}, fopt), vis = torch::empty({P, Ns, 1}, fopt);
+    torch::Tensor diffuse = torch::empty({P, 3}, fopt), local_diffuse = torch::empty({P, 3}, fopt);
+    torch::Tensor accum = torch::empty({P, 1}, fopt), rgb_d = torch::empty({P, 3}, fopt);
+    torch::Tensor rgb_s = torch::empty({P, 3}, fopt);
+    r3dg_brdf_inputs in = brdf_inputs(t, (int)sample_num);
+    r3dg_brdf_complex_outputs o{pbr.data_ptr<float>(),     dirs.data_ptr<float>(),  lights.data_ptr<float>(),
+                                local.data_ptr<float>(),   global.data_ptr<float>(), vis.data_ptr<float>(),
+                                diffuse.data_ptr<float>(), local_diffuse.data_ptr<float>(),
+                                accum.data_ptr<float>(),   rgb_d.data_ptr<float>(), rgb_s.data_ptr<float>()};
+    check(r3dg_render_equation_forward_complex(&in, &o, stream_of(dev)), "render_equation_forward_complex");
+    return {pbr, dirs, lights, local, global, vis, diffuse, local_diffuse, accum, rgb_d, rgb_s};
+}
+
+// RenderEquationBackwardCUDA (render_equation.cu:494-547)
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor,
+           torch::Tensor>
+render_equation_backward(const torch::Tensor& base_color, const torch::Tensor& roughness,
+                         const torch::Tensor& metallic, const torch::Tensor& normals, const torch::Tensor& viewdirs,
+                         const torch::Tensor& incidents_shs, const torch::Tensor& direct_shs,
+                         const torch::Tensor& visibility_shs, int64_t sample_num, const torch::Tensor& incident_dirs,
+                         const torch::Tensor& dL_dpbr, const torch::Tensor& dL_ddiffuse_light, bool debug) {
+    (void)debug;
+    const torch::Device dev = base_color.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    auto t = prep_brdf({base_color, roughness, metallic, normals, viewdirs, incidents_shs, direct_shs, visibility_shs,
+                        incident_dirs, dL_dpbr, dL_ddiffuse_light},
+                       dev);
+    r3dg_brdf_inputs in = brdf_inputs(t, (int)sample_num);
+    const int P = in.P;
+    auto fopt = t[0].options().dtype(torch::kFloat32);
+    torch::Tensor d_base = torch::empty({P, 3}, fopt), d_rough = torch::empty({P, 1}, fopt);
+    torch::Tensor d_metal = torch::empty({P, 1}, fopt), d_n = torch::empty({P, 3}, fopt);
+    torch::Tensor d_v = torch::empty({P, 3}, fopt), d_inc = torch::empty({P, in.S_incident, 3}, fopt);
+    torch::Tensor d_dir = torch::empty({1, in.S_direct, 3}, fopt), d_vis = torch::empty({P, in.S_visibility, 1}, fopt);
+    r3dg_brdf_grads o{d_base.data_ptr<float>(), d_rough.data_ptr<float>(), d_metal.data_ptr<float>(),
+                      d_n.data_ptr<float>(),    d_v.data_ptr<float>(),     d_inc.data_ptr<float>(),
+                      d_dir.data_ptr<float>(),  d_vis.data_ptr<float>()};
+    auto bopt = torch::TensorOptions().dtype(torch::kUInt8).device(dev);
+    TensorAlloc scratch{bopt, torch::empty({0}, bopt)};
+    check(r3dg_render_equation_backward(&in, t[8].data_ptr<float>(), t[9].data_ptr<float>(), t[10].data_ptr<float>(),
+                                        tensor_alloc, &scratch, &o, stream_of(dev)),
+          "render_equation_backward");
+    return {d_base, d_rough, d_metal, d_n, d_v, d_inc, d_dir, d_vis};
+}
+
+std::map<std::string, int64_t> shader_map(int kind) {
+    std::map<std::string, int64_t> m;
+    for (int i = 0; i < r3dg_shader_count(kind); ++i) m[r3dg_shader_name(kind, i)] = r3dg_shader_handle(kind, i);
+    return m;
+}
+
+std::tuple<int64_t, int64_t> preprocess_model(torch::Tensor& xyz) {
+    const torch::Device dev = xyz.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    auto x = dev_contig(xyz, dev);
+    int64_t a = 0, b = 0;
+    check(r3dg_preprocess_model((int)xyz.size(0), x.numel() ? x.data_ptr<float>() : nullptr, &a, &b, stream_of(dev)),
+          "PreprocessModel");
+    return {a, b};
+}
+
+int64_t create_shader_manager(int64_t kind, const torch::Tensor& handles) {
+    auto h = handles.to(torch::kCPU).to(torch::kInt64).contiguous();
+    int64_t m = 0;
+    check(r3dg_create_shader_manager((int)kind, (int)h.numel(), h.data_ptr<int64_t>(), &m,
+                                     stream_of(torch::Device(torch::kCUDA, c10::hip::current_device()))),
+          "create_shader_manager");
+    return m;
+}
+
+std::tuple<std::vector<int64_t>, std::vector<int64_t>> shader_manager_info(int64_t mgr) {
+    int n = 0;
+    check(r3dg_shader_manager_info(mgr, &n, nullptr, nullptr), "shader_manager_info");
+    std::vector<int64_t> h(n);
+    std::vector<int> c(n);
+    check(r3dg_shader_manager_info(mgr, &n, h.data(), c.data()), "shader_manager_info");
+    return {h, std::vector<int64_t>(c.begin(), c.end())};
+}
+
+int64_t allocate_texture(const std::map<std::string, torch::Tensor>&) {
+    throw std::runtime_error(
+        "AllocateTexture: the texture manager serves only the non-default shader library, which is the next row "
+        "of this build's scope (DESIGN.md 'Scope'); default shaders need no textures");
+}
+int64_t upload_textures(const std::vector<std::string>&, const std::vector<int64_t>&, int64_t) {
+    throw std::runtime_error(
+        "UploadTexturesToDevice: the texture manager is not in this build's scope yet (DESIGN.md 'Scope')");
+}
+
+// parity / debug accessor: views of the sorted keys, point list, tile ranges and per-Gaussian state
+std::vector<torch::Tensor> rasterizer_state(const torch::Tensor& geomBuffer, const torch::Tensor& binningBuffer,
+                                            const torch::Tensor& imageBuffer, int64_t P, int64_t H, int64_t W,
+                                            int64_t L) {
+    r3dg_binning_view v{};
+    check(r3dg_state_view((int)P, (int)H, (int)W, (int)L, geomBuffer.data_ptr(), binningBuffer.data_ptr(),
+                          imageBuffer.data_ptr(), &v),
+          "rasterizer_state");
+    auto slice = [](const torch::Tensor& buf, const void* p, int64_t nbytes) {
+        const int64_t off = (const char*)p - (const char*)buf.data_ptr();
+        return buf.narrow(0, off, nbytes);
+    };
+    const int64_t T = ((W + 15) / 16) * ((H + 15) / 16);
+    return {slice(binningBuffer, v.keys_sorted, 8 * L).view(torch::kInt64),
+            slice(binningBuffer, v.point_list, 4 * L).view(torch::kInt32),
+            slice(imageBuffer, v.ranges, 8 * T).view(torch::kInt32).view({T, 2}),
+            slice(geomBuffer, v.point_offsets, 4 * P).view(torch::kInt32),
+            slice(geomBuffer, v.depths, 4 * P).view(torch::kFloat32),
+            slice(geomBuffer, v.means2D, 8 * P).view(torch::kFloat32).view({P, 2}),
+            slice(geomBuffer, v.conic_opacity, 16 * P).view(torch::kFloat32).view({P, 4}),
+            slice(geomBuffer, v.rgb, 12 * P).view(torch::kFloat32).view({P, 3}),
+            slice(geomBuffer, v.cov3D, 24 * P).view(torch::kFloat32).view({P, 6}),
+            slice(geomBuffer, v.clamped, P)};
+}
+
+std::vector<int64_t> feature_groups(int64_t S) {
+    int g[64];
+    const int n = r3dg_feature_groups((int)S, g);
+    return std::vector<int64_t>(g, g + n);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+    m.doc() = "MI355X-native relightable Gaussian-splat rasterizer (drop-in for r3dg_rasterization._C)";
+    // the reference surface (ext.cu:21-35)
+    m.def("rasterize_gaussians", &rasterize_gaussians);
+    m.def("rasterize_gaussians_backward", &rasterize_gaussians_backward);
+    m.def("render_equation_forward", &render_equation_forward);
+    m.def("render_equation_forward_complex", &render_equation_forward_complex);
+    m.def("render_equation_backward", &render_equation_backward);
+    m.def("mark_visible", &mark_visible);
+    m.def("GetSplatShaderAddressMap", []() { return shader_map(R3DG_SHADER_SPLAT); });
+    m.def("GetShShaderAddressMap", []() { return shader_map(R3DG_SHADER_SH); });
+    m.def("GetPostProcessShaderAddressMap", []() { return shader_map(R3DG_SHADER_POST); });
+    m.def("PreprocessModel", &preprocess_model);
+    m.def("EncodeTextureMode", [](const std::string& s) { return r3dg_encode_texture_mode(s.c_str()); });
+    m.def("EncodeWrapMode", [](const std::string& s) { return r3dg_encode_wrap_mode(s.c_str()); });
+    m.def("AllocateTexture", &allocate_texture);
+    m.def("UploadTexturesToDevice", &upload_textures);
+    // extensions
+    m.def("rasterize_gaussians_backward_ex", &rasterize_gaussians_backward_ex);
+    m.def("render_equation_forward_with_rand", &render_equation_forward_with_rand);
+    m.def("rasterizer_state", &rasterizer_state);
+    m.def("feature_groups", &feature_groups);
+    m.def("create_shader_manager", &create_shader_manager);
+    m.def("shader_manager_info", &shader_manager_info);
+    m.def("abi_version", []() { return r3dg_abi_version(); });
+}

@@ -1,0 +1,84 @@
+"""Shared helpers: run the HIP path through `_C` exactly as the reference call sites do."""
+from __future__ import annotations
+
+import numpy as np
+
+
+def tt(a, device="cuda"):
+    import torch
+
+    if a is None:
+        return torch.empty(0, device=device)
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32, device=device)
+
+
+def hip_forward(_C, scene, cam, S=None, degree=3, bg=(1.0, 1.0, 1.0), use_sh=True, use_cov=False, colors=None,
+                scale_modifier=1.0, pseudo_normal=True, features=None):
+    """Call _C.rasterize_gaussians with the argument order of rasterize_points.cu:39-71."""
+    import torch
+
+    feats = scene.features if features is None else features
+    if S is not None:
+        feats = feats[:, :S]
+    cov = None
+    if use_cov:
+        import oracle
+
+        cov = oracle.cov3d(scene.scales, scene.rotations, scale_modifier)
+    args = dict(
+        means3D=tt(scene.means3D), features=tt(np.ascontiguousarray(feats)),
+        colors=tt(colors) if colors is not None else tt(None), opacity=tt(scene.opacity),
+        scales=tt(None) if use_cov else tt(scene.scales), rotations=tt(None) if use_cov else tt(scene.rotations),
+        cov3D=tt(cov) if use_cov else tt(None), sh=tt(scene.sh) if (use_sh and colors is None) else tt(None))
+    out = _C.rasterize_gaussians(
+        tt(bg), 0.0, 0.0, args["means3D"], args["features"], args["colors"], args["opacity"], args["scales"],
+        args["rotations"], scale_modifier, args["cov3D"], tt(cam.view), tt(cam.view_inv), tt(cam.proj),
+        tt(cam.proj_inv), cam.tanfovx, cam.tanfovy, cam.cx, cam.cy, cam.height, cam.width, args["sh"], degree,
+        tt(cam.campos), False, pseudo_normal, None, None, None, None, False)
+    names = ["num_rendered", "n_contrib", "color", "opacity", "depth", "stencil", "feature", "shader_color", "normal",
+             "surface_xyz", "radii", "geom", "binning", "image"]
+    res = dict(zip(names, out))
+    res["_args"] = args
+    res["_cam"] = cam
+    res["_degree"] = degree
+    res["_bg"] = bg
+    res["_scale_modifier"] = scale_modifier
+    torch.cuda.synchronize()
+    return res
+
+
+def hip_backward(_C, fwd, dcolor_chw, dopac, ddepth, dfeat_planar, backward_geometry=True):
+    """_C.rasterize_gaussians_backward with the reference's CHW / planar grad contract."""
+    a = fwd["_args"]
+    cam = fwd["_cam"]
+    out = _C.rasterize_gaussians_backward(
+        tt(fwd["_bg"]), a["means3D"], a["features"], fwd["radii"], a["colors"], a["scales"], a["rotations"],
+        fwd["_scale_modifier"], a["cov3D"], tt(cam.view), tt(cam.proj), cam.tanfovx, cam.tanfovy, tt(dcolor_chw),
+        tt(dopac), tt(ddepth), tt(dfeat_planar), a["sh"], fwd["_degree"], tt(cam.campos), fwd["geom"],
+        fwd["num_rendered"], fwd["binning"], fwd["image"], backward_geometry, False)
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dfeatures", "dL_dcov3D", "dL_dsh",
+             "dL_dscales", "dL_drotations"]
+    return {k: v.detach().cpu().numpy() for k, v in zip(names, out)}
+
+
+def upstream_grads(H, W, S, seed=1, scale=1e-3):
+    rng = np.random.default_rng(seed)
+    f = lambda *s: (rng.normal(size=s) * scale).astype(np.float32)  # noqa: E731
+    return f(3, H, W), f(H * W), f(H * W), f(S, H, W)
+
+
+def close(a, b, atol, rtol=0.0):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    err = np.abs(a - b) - (atol + rtol * np.abs(b))
+    return float(err.max()) if err.size else 0.0
+
+
+def assert_close(name, a, b, atol, rtol=0.0):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, f"{name}: shape {a.shape} vs {b.shape}"
+    d = np.abs(a.astype(np.float64) - b.astype(np.float64))
+    bad = d > (atol + rtol * np.abs(b.astype(np.float64)))
+    assert not bad.any(), (f"{name}: {int(bad.sum())}/{bad.size} elements off, max abs diff {d.max():.3e} "
+                           f"(atol {atol}, rtol {rtol}) at {np.unravel_index(np.argmax(d), d.shape)}")
