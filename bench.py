@@ -1,0 +1,214 @@
+"""Benchmark of the hot path: rasterize_gaussians + rasterize_gaussians_backward (Mpix/s fwd+bwd).
+
+Workload (BASELINE.json metric, SURVEY.md §8d "M1"): 1,000,000 synthetic Gaussians, 1920x1080,
+S=11 features, SH degree 3, default shaders, pseudo normal on, backward_geometry on; upstream
+gradients N(0,1)*1e-3 in the reference's CHW contract. One step = one view: the reference's
+`_C.rasterize_gaussians` then `_C.rasterize_gaussians_backward` through this build's `_C`, and,
+when N > 1, one RCCL all-reduce of the flat per-Gaussian gradient buffer (70 floats/Gaussian:
+means3D 3 + sh 48 + opacity 1 + scales 3 + rotations 4 + features 11) -- view-parallel data
+parallelism, every rank renders its own camera of the same scene (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Rank 0 prints one JSON line. `roofline` prices the tile-blend kernels (render fwd + render bwd)
+with SURVEY.md §8d's algorithmic bytes (272*L + 156*H*W + 16*tiles at S=11) over their HIP-event
+device time measured on the launch stream during the timed steps; `traffic` is the HBM bytes of
+the same two kernels from rocprofv3 PMC counters (profiles/, FETCH_SIZE doubled per
+MI355X_MICROARCH.md §HBM), or null. `cpu_baseline` times the CPU oracle (a scalar C port of the
+reference path) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+P_M1, W_M1, H_M1, S_M1 = 1_000_000, 1920, 1080, 11
+
+
+def algorithmic_bytes(L: int, npix: int, tiles: int, S: int) -> tuple[int, int]:
+    """SURVEY.md §8d per-unit figures: fwd L*(56+4S) + Npix*(40+4S) + 8T, bwd L*(84+8S) + Npix*(28+4S) + 8T."""
+    fwd = L * (56 + 4 * S) + npix * (40 + 4 * S) + 8 * tiles
+    bwd = L * (84 + 8 * S) + npix * (28 + 4 * S) + 8 * tiles
+    return fwd, bwd
+
+
+def rank_camera(rank: int, world: int):
+    from relightable3dgaussian_amd import synthetic
+
+    cam = synthetic.m1_camera(W_M1, H_M1)
+    if world == 1:
+        return cam
+    yaw = math.radians((rank - (world - 1) / 2.0) * 1.0)  # small per-rank yaw: similar cost per view
+    R = np.array([[math.cos(yaw), 0, math.sin(yaw)], [0, 1, 0], [-math.sin(yaw), 0, math.cos(yaw)]])
+    return synthetic.make_camera(R, np.zeros(3), cam.fovx, cam.fovy, W_M1, H_M1)
+
+
+def load_traffic() -> dict | None:
+    path = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def cpu_baseline(scene) -> dict:
+    """The CPU oracle on a bounded sample of the M1 workload: the full 1M-Gaussian scene seen by a
+    central 960x544 window of the same camera (same focal length), fwd + bwd, one thread."""
+    import oracle
+    from relightable3dgaussian_amd import synthetic
+
+    full = synthetic.m1_camera(W_M1, H_M1)
+    fx, fy = full.focal
+    w, h = 960, 544
+    cam = synthetic.make_camera(np.eye(3), np.zeros(3), 2 * math.atan(w / 2 / fx), 2 * math.atan(h / 2 / fy), w, h)
+    rng = np.random.default_rng(1)
+    dc = (rng.normal(size=(3, h, w)) * 1e-3).astype(np.float32)
+    do = (rng.normal(size=h * w) * 1e-3).astype(np.float32)
+    dd = (rng.normal(size=h * w) * 1e-3).astype(np.float32)
+    df = (rng.normal(size=(S_M1, h, w)) * 1e-3).astype(np.float32)
+    oracle.build()
+    t0 = time.perf_counter()
+    o = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features, sh=scene.sh, scales=scene.scales,
+                                 rotations=scene.rotations)
+    oracle.rasterize_backward(o, dc, do, dd, df)
+    dt = time.perf_counter() - t0
+    return {"value": round(w * h / dt / 1e6, 6), "unit": "Mpix/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/r3dg_oracle.c (scalar C port), M1 scene (1M Gaussians) through a central {w}x{h} "
+                      f"window of the metric camera, preprocess+sort+blend fwd+bwd, {dt:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--P", type=int, default=P_M1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    import relightable3dgaussian_amd as r3
+    from relightable3dgaussian_amd import synthetic
+
+    _C = r3._C
+    cam = rank_camera(rank, world)
+    scene = synthetic.m1_scene(P=args.P, S=S_M1, seed=0, cam=synthetic.m1_camera(W_M1, H_M1))
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32, device=dev)  # noqa: E731
+    means3D, feats, opac = t(scene.means3D), t(scene.features), t(scene.opacity)
+    scales, rots, sh = t(scene.scales), t(scene.rotations), t(scene.sh)
+    empty = torch.empty(0, device=dev)
+    bg = t([1.0, 1.0, 1.0])
+    view, view_inv, proj, proj_inv, campos = t(cam.view), t(cam.view_inv), t(cam.proj), t(cam.proj_inv), t(cam.campos)
+    H, W = cam.height, cam.width
+    rng = np.random.default_rng(1)
+    g_color = t(rng.normal(size=(3, H, W)) * 1e-3)
+    g_opac = t(rng.normal(size=(H, W)) * 1e-3)
+    g_depth = t(rng.normal(size=(H, W)) * 1e-3)
+    g_feat = t(rng.normal(size=(S_M1, H, W)) * 1e-3)
+
+    def step():
+        out = _C.rasterize_gaussians(bg, 0.0, 0.0, means3D, feats, empty, opac, scales, rots, 1.0, empty, view,
+                                     view_inv, proj, proj_inv, cam.tanfovx, cam.tanfovy, cam.cx, cam.cy, H, W, sh, 3,
+                                     campos, False, True, None, None, None, None, False)
+        L, radii, geom, binning, img = out[0], out[10], out[11], out[12], out[13]
+        grads = _C.rasterize_gaussians_backward(bg, means3D, feats, radii, empty, scales, rots, 1.0, empty, view,
+                                                proj, cam.tanfovx, cam.tanfovy, g_color, g_opac, g_depth, g_feat,
+                                                sh, 3, campos, geom, L, binning, img, True, False)
+        if world > 1:
+            # grads: means2D, colors, opacity, means3D, features, cov3D, sh, scales, rotations
+            flat = torch.cat([grads[3].reshape(-1), grads[6].reshape(-1), grads[2].reshape(-1),
+                              grads[7].reshape(-1), grads[8].reshape(-1), grads[4].reshape(-1)])
+            dist.all_reduce(flat)
+        return L
+
+    for _ in range(args.warmup):
+        L = step()
+    torch.cuda.synchronize()
+    _C.profile_enable(args.steps + 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        L = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = {k: _C.profile_read(i) for i, k in enumerate(["render_fwd", "render_bwd", "gather_bwd", "sort",
+                                                          "preprocess"])}
+    _C.profile_enable(0)
+    if world > 1:
+        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = float(te.item())
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    ms_step = elapsed / args.steps * 1e3
+    npix = H * W
+    value = world * npix * args.steps / elapsed / 1e6
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    bf, bb = algorithmic_bytes(L, npix, tiles, S_M1)
+    avg = {k: (v[1] / v[0] if v[0] else float("nan")) for k, v in prof.items()}
+    t_kern = (avg["render_fwd"] + avg["render_bwd"]) / 1e3
+    achieved = (bf + bb) / t_kern / 1e9
+    traffic = None
+    tr = load_traffic()
+    if tr and tr.get("config") == f"M1 P={args.P}":
+        traffic = tr.get("render_fwd_bytes", 0) + tr.get("render_bwd_bytes", 0)
+    res = {
+        "metric": "Mpix/s fwd+bwd, 1M Gaussians @1920x1080; views/s at 1/2/4/8 MI355X",
+        "value": round(value, 3),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SURVEY.md §8d M1 generator, seed 0; no datasets offline)",
+        "config": {"workload": "M1: rasterize_gaussians + rasterize_gaussians_backward, 1M Gaussians, 1920x1080, "
+                               "S=11 features, SH degree 3, default shaders, pseudo normal",
+                   "gaussians": args.P, "width": W, "height": H, "features": S_M1, "num_rendered": int(L),
+                   "parallelism": f"view-parallel dp{world} (RCCL all-reduce of 70 floats/Gaussian)"},
+        "views_per_s": round(world * args.steps / elapsed, 3),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "render_fwd_kernel + render_bwd_kernel (tile blend)",
+                     "algorithmic_bytes": bf + bb, "kernel_ms": round(t_kern * 1e3, 4)},
+        "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        res["cpu_baseline"] = cpu_baseline(scene)
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -233,6 +233,16 @@ int r3dg_create_shader_manager(int kind, int P, const int64_t* shader_handles_ho
                                r3dg_stream_t stream);
 int r3dg_shader_manager_info(int64_t manager, int* n_shaders, int64_t* handles, int* instance_counts);
 
+/* ---- profiling ------------------------------------------------------------------------------ */
+/* When enabled, HIP events are recorded on the caller's stream immediately before and after the
+ * tile-blend kernels (the roofline kernels of DESIGN.md), up to max_records launches each.
+ * r3dg_profile_read synchronises on the recorded events, returns the launch count and summed
+ * device time in ms for one kernel, and resets that kernel's records. */
+enum { R3DG_PROF_RENDER_FWD = 0, R3DG_PROF_RENDER_BWD = 1, R3DG_PROF_GATHER_BWD = 2, R3DG_PROF_SORT = 3,
+       R3DG_PROF_PREPROCESS = 4, R3DG_PROF_KINDS = 5 };
+int r3dg_profile_enable(int max_records);
+int r3dg_profile_read(int kernel, int* count, float* total_ms);
+
 /* Texture mode helpers (utils/texture.cu EncodeTextureMode / EncodeWrapMode). */
 int r3dg_encode_texture_mode(const char* mode);
 int r3dg_encode_wrap_mode(const char* mode);

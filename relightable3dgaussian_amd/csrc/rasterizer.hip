@@ -134,6 +134,30 @@ size_t image_state_bytes(int H, int W) {
 }
 ImageState image_state_from(void* base, int H, int W) { return carve_image((uintptr_t)base, H, W, nullptr); }
 
+// ---- profiling events (r3dg_profile_*) -----------------------------------------------------------
+struct Profiler {
+    int max_records = 0;
+    std::vector<hipEvent_t> ev[R3DG_PROF_KINDS][2];
+    int n[R3DG_PROF_KINDS] = {0};
+};
+static Profiler g_prof;
+static std::mutex g_prof_mu;
+
+struct ProfScope {
+    int k;
+    hipStream_t st;
+    int idx = -1;
+    ProfScope(int kind, hipStream_t s) : k(kind), st(s) {
+        if (g_prof.max_records > 0 && g_prof.n[k] < g_prof.max_records) {
+            idx = g_prof.n[k]++;
+            (void)hipEventRecord(g_prof.ev[k][0][idx], st);
+        }
+    }
+    ~ProfScope() {
+        if (idx >= 0) (void)hipEventRecord(g_prof.ev[k][1][idx], st);
+    }
+};
+
 // rasterizer_impl.cu:37-52
 static uint32_t higher_msb(uint32_t n) {
     uint32_t msb = sizeof(n) * 4, step = msb;
@@ -324,7 +348,10 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         pa.radii = radii; pa.tiles_touched = geom.tiles_touched; pa.depths = geom.depths;
         pa.means2D = geom.means2D; pa.cov3D = geom.cov3D; pa.conic_opacity = geom.conic_opacity;
         pa.rgb = geom.rgb; pa.clamped = geom.clamped; pa.error_flag = nullptr;
-        hipLaunchKernelGGL(preprocess_kernel, dim3((P + 255) / 256), dim3(256), 0, st, pa);
+        {
+            ProfScope ps(R3DG_PROF_PREPROCESS, st);
+            hipLaunchKernelGGL(preprocess_kernel, dim3((P + 255) / 256), dim3(256), 0, st, pa);
+        }
         R3DG_CHECK_LAUNCH(s->debug, st);
 
         size_t tb = geom.scan_temp_bytes;
@@ -350,9 +377,12 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         R3DG_CHECK_LAUNCH(s->debug, st);
         const int bit = (int)higher_msb((uint32_t)T);
         size_t sb = bin.sort_temp_bytes;
-        R3DG_CHECK_HIP(rocprim::radix_sort_pairs(bin.sort_temp, sb, bin.keys_unsorted, bin.keys_sorted,
-                                                 rocprim::counting_iterator<uint32_t>(0), bin.sorted_slot,
-                                                 (size_t)L, 0, 32 + bit, st));
+        {
+            ProfScope ps(R3DG_PROF_SORT, st);
+            R3DG_CHECK_HIP(rocprim::radix_sort_pairs(bin.sort_temp, sb, bin.keys_unsorted, bin.keys_sorted,
+                                                     rocprim::counting_iterator<uint32_t>(0), bin.sorted_slot,
+                                                     (size_t)L, 0, 32 + bit, st));
+        }
         hipLaunchKernelGGL(identify_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, st, L, bin.keys_sorted,
                            bin.sorted_slot, bin.gid_of_slot, bin.point_list, img.ranges);
         R3DG_CHECK_LAUNCH(s->debug, st);
@@ -381,7 +411,10 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     ra.out_shader_color = out->shader_color;
     ra.flay = make_feature_layout(S, (long long)H * W, true);
     if (const char* e = getenv("R3DG_NO_CULL")) ra.cull = (e[0] == '0');
-    R3DG_CHECK_HIP(launch_render_forward(ra, false, st));
+    {
+        ProfScope ps(R3DG_PROF_RENDER_FWD, st);
+        R3DG_CHECK_HIP(launch_render_forward(ra, false, st));
+    }
     R3DG_CHECK_LAUNCH(s->debug, st);
 
     if (s->compute_pseudo_normal) {
@@ -471,7 +504,10 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         ba.backward_geometry = backward_geometry;
         ba.RS = RS;
         ba.rows = rows;
-        R3DG_CHECK_HIP(launch_render_backward(ba, st));
+        {
+            ProfScope ps(R3DG_PROF_RENDER_BWD, st);
+            R3DG_CHECK_HIP(launch_render_backward(ba, st));
+        }
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
     GatherBwdArgs ga{};
@@ -504,7 +540,10 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     ga.dL_dscales = out->dL_dscales;
     ga.dL_drotations = out->dL_drotations;
     if (!g->sh) ga.sh = nullptr;
-    R3DG_CHECK_HIP(launch_gather_backward(ga, st));
+    {
+        ProfScope ps(R3DG_PROF_GATHER_BWD, st);
+        R3DG_CHECK_HIP(launch_gather_backward(ga, st));
+    }
     R3DG_CHECK_LAUNCH(s->debug, st);
     return R3DG_OK;
 }
@@ -594,4 +633,39 @@ extern "C" int r3dg_encode_wrap_mode(const char* mode) {
     if (!strcmp(mode, "Mirror")) return (int)hipAddressModeMirror;
     if (!strcmp(mode, "Wrap")) return (int)hipAddressModeWrap;
     return -1;
+}
+
+extern "C" int r3dg_profile_enable(int max_records) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (int k = 0; k < R3DG_PROF_KINDS; ++k) {
+        for (int e = 0; e < 2; ++e) {
+            for (hipEvent_t ev : g_prof.ev[k][e]) R3DG_CHECK_HIP(hipEventDestroy(ev));
+            g_prof.ev[k][e].clear();
+        }
+        g_prof.n[k] = 0;
+    }
+    g_prof.max_records = max_records > 0 ? max_records : 0;
+    for (int k = 0; k < R3DG_PROF_KINDS; ++k)
+        for (int e = 0; e < 2; ++e) {
+            g_prof.ev[k][e].resize(g_prof.max_records);
+            for (auto& ev : g_prof.ev[k][e]) R3DG_CHECK_HIP(hipEventCreate(&ev));
+        }
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_profile_read(int kernel, int* count, float* total_ms) {
+    R3DG_REQUIRE(kernel >= 0 && kernel < R3DG_PROF_KINDS && count && total_ms, "profile_read: bad arguments");
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    float sum = 0.f;
+    const int n = g_prof.n[kernel];
+    for (int i = 0; i < n; ++i) {
+        R3DG_CHECK_HIP(hipEventSynchronize(g_prof.ev[kernel][1][i]));
+        float ms = 0.f;
+        R3DG_CHECK_HIP(hipEventElapsedTime(&ms, g_prof.ev[kernel][0][i], g_prof.ev[kernel][1][i]));
+        sum += ms;
+    }
+    g_prof.n[kernel] = 0;
+    *count = n;
+    *total_ms = sum;
+    return R3DG_OK;
 }

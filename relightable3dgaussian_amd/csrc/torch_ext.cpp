@@ -487,4 +487,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("create_shader_manager", &create_shader_manager);
     m.def("shader_manager_info", &shader_manager_info);
     m.def("abi_version", []() { return r3dg_abi_version(); });
+    m.def("profile_enable", [](int64_t n) { check(r3dg_profile_enable((int)n), "profile_enable"); });
+    m.def("profile_read", [](int64_t kernel) {
+        int c = 0;
+        float ms = 0.f;
+        check(r3dg_profile_read((int)kernel, &c, &ms), "profile_read");
+        return std::make_tuple((int64_t)c, (double)ms);
+    });
 }
