@@ -46,7 +46,7 @@ __device__ __forceinline__ int wave_max_int(int v) {
 }
 
 template <int SMAX>
-__global__ void __launch_bounds__(kBlock) render_bwd_kernel(RenderBwdArgs a) {
+__global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a) {
     constexpr int NA4 = (4 + SMAX + 3) / 4;      // attribute row: colour, depth, features
     constexpr int NR = kRowFeat + SMAX;          // reduced values per instance
     constexpr int RSL = (NR + 3) & ~3;           // LDS partial row stride (floats)
@@ -240,9 +240,330 @@ __global__ void __launch_bounds__(kBlock) render_bwd_kernel(RenderBwdArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// MFMA variant of the backward blend.
+//
+// Every per-pixel contribution of one instance is linear in two per-pixel scalars:
+//   w = alpha*T          -> colour (w*g_c), feature (w*gf_c) and depth (w*gd) gradients;
+//   q = G*dL_dalpha      -> opacity (q), and mean2D / conic gradients through the moments
+//                           sum q * {1, x, y, x^2, xy, y^2} of tile-centred pixel coordinates
+//                           (dx = d0x - x with d0x the centre offset; expanded at the flush).
+// So a wave's reduction over its 64 pixels for 16 instances is two small matrix products,
+// [16 inst x 64 px] @ [64 px x 16 ch], done with v_mfma_f32_16x16x4_f32 (exact f32 fma
+// chains): per 16 instances 16 MFMAs per 16-channel block instead of (10+S)*6 DPP ops per
+// instance. w and q go through a padded LDS image (row stride 66 floats: conflict-free for
+// both the row-wise writes and the column-wise A-operand reads).
+// ---------------------------------------------------------------------------------------------
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// Order this wave's LDS traffic for cross-lane exchange through LDS: wait for the wave's DS
+// operations and stop the compiler from moving memory accesses across (it cannot see lanes).
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int SMAX>
+__global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a) {
+    constexpr int NA4 = (4 + SMAX + 3) / 4;       // staged attribute row: colour, depth, features
+    constexpr int NR = kRowFeat + SMAX;
+    constexpr int RSL = (NR + 3) & ~3;            // LDS partial row stride (floats)
+    constexpr int CH = 32;                        // instances per flush chunk (= one compaction mask)
+    constexpr int NXB = (4 + SMAX + 15) / 16;     // 16-channel blocks of X = [g0..2, gf0..S-1, gd]
+    constexpr int WQS = 66;                       // padded LDS row stride of the w|q image
+    constexpr int GRP = 8;                        // instances per MFMA group: rows 0..7 w, 8..15 q
+    __shared__ float2 s_xy[kBlock];
+    __shared__ float4 s_co[kBlock];
+    __shared__ uint32_t s_slot[kBlock];
+    __shared__ float4 s_attr[kBlock * NA4];
+    __shared__ uint32_t s_bits[8][4];             // [chunk][wave] live-instance masks
+    __shared__ float4 s_part4[4 * CH * RSL / 4];  // [wave][chunk instance][RSL]
+    __shared__ float s_wq[4][16 * WQS];           // per wave: rows 0..7 w, 8..15 q; [row][pixel]
+    __shared__ int s_rowid[4][GRP];
+    __shared__ int s_max_last;
+    float* s_part = reinterpret_cast<float*>(s_part4);
+
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (tile >= a.num_tiles) return;
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
+    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const int pix = inside ? py * a.W + px : 0;
+    const float pfx = (float)px, pfy = (float)py;
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+    const int S = a.S;
+
+    const float T_final = inside ? a.final_T[pix] : 0.f;
+    float T = T_final;
+    const int last = inside ? (int)a.n_contrib[pix] : 0;
+    float g[3], gf[SMAX > 0 ? SMAX : 1], gd = 0.f, go = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) g[c] = inside ? a.dL_dpix[a.ca[c] + pix * a.cm[c]] : 0.f;
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c) gf[c] = (inside && c < S) ? a.dL_dpix_f[a.gflay.a[c] + pix * a.gflay.m[c]] : 0.f;
+    if (inside) {
+        gd = a.dL_dpix_d[pix];
+        go = a.dL_dpix_o[pix];
+    }
+    const float bg_dot = a.bg[0] * g[0] + a.bg[1] * g[1] + a.bg[2] * g[2];
+
+    // ---- B operands: X[pixel][channel] and Y[pixel][moment] for k-step s (pixel 4s + (l>>4)) ----
+    float* wq = s_wq[w];
+    float bX[NXB][16];
+    float bY[16];
+    {
+#pragma unroll
+        for (int xb = 0; xb < NXB; ++xb) {
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                const int ch = xb * 16 + c;
+                float v = 0.f;
+                if (ch < 3) v = g[ch];
+                else if (ch - 3 < SMAX && ch - 3 < S) v = gf[(ch - 3) < SMAX ? (ch - 3) : 0];
+                else if (ch == 3 + S) v = gd;
+                wq[c * WQS + l] = v;
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
+            wave_lds_sync();
+        }
+        const int nch = l & 15;
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+            const int pl = 4 * s2 + (l >> 4);  // pixel lane of k-step s2
+            const float xo = (float)((w & 1) * 8 + (pl & 7)) - 7.5f;
+            const float yo = (float)((w >> 1) * 8 + (pl >> 3)) - 7.5f;
+            float v = 0.f;
+            v = nch == 0 ? 1.f : v;
+            v = nch == 1 ? xo : v;
+            v = nch == 2 ? yo : v;
+            v = nch == 3 ? xo * xo : v;
+            v = nch == 4 ? xo * yo : v;
+            v = nch == 5 ? yo * yo : v;
+            bY[s2] = v;
+        }
+    }
+
+    // The reference keeps one accum_rec per channel (colour, features, depth); all share the same
+    // alpha recurrence and enter dL/dalpha only through their dot with the upstream gradient, so one
+    // scalar acc_dot = sum_c accum_rec[c] * dL_dchannel[c] carries them all.
+    if (!a.backward_geometry) {
+#pragma unroll
+        for (int c = 0; c < SMAX; ++c) gf[c] = 0.f;  // bX already holds the feature grads
+    }
+    float acc_dot = 0.f, last_dot = 0.f, acc_o = 0.f, last_alpha = 0.f;
+
+    const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
+    if (t == 0) s_max_last = 0;
+    for (int i = t; i < 4 * CH * RSL / 4; i += kBlock) s_part4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    if (l == 0) atomicMax(&s_max_last, wmax);
+    __syncthreads();
+    const int max_last = s_max_last;
+    const int RS = a.RS;
+    for (int p = max_last + t; p < n; p += kBlock) {
+        float4* row = reinterpret_cast<float4*>(a.rows + (size_t)a.sorted_slot[range.x + p] * RS);
+        for (int q = 0; q < RS / 4; ++q) row[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // partial-row slot of each X channel / Y moment (col l&15 of the MFMA result)
+    const int nch = l & 15;
+    int xslot[NXB];
+#pragma unroll
+    for (int xb = 0; xb < NXB; ++xb) {
+        const int ch = xb * 16 + nch;
+        xslot[xb] = ch < 3 ? kRowColor + ch : (ch - 3 < S ? kRowFeat + (ch - 3) : (ch == 3 + S ? kRowMean + 2 : -1));
+    }
+    // moments: S0 -> opacity slot, Sx, Sy, Sxx, Sxy, Syy -> mean x, mean y, conic x, y, w slots
+    const int yslot = nch == 0 ? kRowOpacity : (nch == 1 ? 0 : (nch == 2 ? 1 : (nch < 6 ? nch : -1)));
+    const float ctx = (float)(tx * kTileX) + 7.5f, cty = (float)(ty * kTileY) + 7.5f;
+    const bool x_half = (l >> 4) < 2;  // result rows 0..7 (w . X) live in lanes 0..31, 8..15 (q . Y) in 32..63
+
+    for (int hi = max_last; hi > 0; hi -= kBlock) {
+        const int cnt = min(kBlock, hi);
+        __syncthreads();
+        uint32_t m = 0;
+        if (t < cnt) {
+            const uint32_t k = range.x + (uint32_t)(hi - 1 - t);
+            const uint32_t gid = a.point_list[k];
+            s_slot[t] = a.sorted_slot[k];
+            const float2 xy = a.means2D[gid];
+            const float4 co = a.conic_opacity[gid];
+            s_xy[t] = xy;
+            s_co[t] = co;
+            m = quadrant_mask_b(xy, co, tx * kTileX, ty * kTileY, a.cull);
+            float v[NA4 * 4];
+#pragma unroll
+            for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
+            v[0] = a.colors[3 * gid + 0];
+            v[1] = a.colors[3 * gid + 1];
+            v[2] = a.colors[3 * gid + 2];
+            v[3] = a.depths[gid];
+            const float* f = a.features + (size_t)gid * S;
+#pragma unroll
+            for (int c = 0; c < SMAX; ++c)
+                if (c < S) v[4 + c] = f[c];
+#pragma unroll
+            for (int q = 0; q < NA4; ++q)
+                s_attr[t * NA4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const unsigned long long bal = __ballot((m >> b) & 1u);
+            if (l == 0) {
+                s_bits[2 * w][b] = (uint32_t)bal;
+                s_bits[2 * w + 1][b] = (uint32_t)(bal >> 32);
+            }
+        }
+        __syncthreads();
+        const int jmin = hi - wmax;  // instances j < jmin lie beyond every pixel of this wave
+        for (int c = 0; c * CH < cnt; ++c) {
+            uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[c][w]);
+            const int lo = jmin - c * CH;
+            if (lo >= CH) bits = 0;
+            else if (lo > 0) bits &= ~0u << lo;
+            int r = 0;  // rows filled in the current MFMA group
+            while (bits) {
+                const int jj = __builtin_ctz(bits);
+                bits &= bits - 1;
+                const int j = c * CH + jj;
+                const int p = hi - 1 - j;  // position in the tile range (reference `contributor`)
+                float wv = 0.f, qv = 0.f;
+                if (inside && p < last) {
+                    const float2 xy = s_xy[j];
+                    const float4 co = s_co[j];
+                    const float dx = xy.x - pfx, dy = xy.y - pfy;
+                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    if (!(power > 0.0f)) {
+                        const float G = __expf(power);
+                        const float alpha = fminf(0.99f, co.w * G);
+                        if (!(alpha < 1.0f / 255.0f)) {
+                            const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
+                            T = T * rinv;
+                            const float dchannel_dcolor = alpha * T;
+                            float v[NA4 * 4];
+#pragma unroll
+                            for (int q = 0; q < NA4; ++q) {
+                                const float4 rr = s_attr[j * NA4 + q];
+                                v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
+                            }
+                            float dot = v[0] * g[0] + v[1] * g[1] + v[2] * g[2] + v[3] * gd;
+#pragma unroll
+                            for (int c2 = 0; c2 < SMAX; ++c2) dot += v[4 + c2] * gf[c2];
+                            acc_dot = last_alpha * last_dot + (1.f - last_alpha) * acc_dot;
+                            last_dot = dot;
+                            float dL_dalpha = dot - acc_dot;
+                            acc_o = last_alpha + (1.f - last_alpha) * acc_o;
+                            dL_dalpha += (1.0f - acc_o) * go;
+                            dL_dalpha *= T;
+                            last_alpha = alpha;
+                            dL_dalpha += (-T_final * rinv) * bg_dot;
+                            wv = dchannel_dcolor;
+                            qv = G * dL_dalpha;
+                        }
+                    }
+                }
+                wq[r * WQS + l] = wv;
+                wq[(GRP + r) * WQS + l] = qv;
+                if (l == 0) s_rowid[w][r] = jj;
+                ++r;
+                if (r == GRP || bits == 0) {
+                    // [8 w rows | 8 q rows] x [64 px] against X (16 ch) and Y (moments): rows 0..7
+                    // of w.X and rows 8..15 of q.Y are the useful halves
+                    wave_lds_sync();
+                    floatx4 accX[NXB], accY = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int xb = 0; xb < NXB; ++xb) accX[xb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s2 = 0; s2 < 16; ++s2) {
+                        const float av = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
+#pragma unroll
+                        for (int xb = 0; xb < NXB; ++xb)
+                            accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
+                        accY = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bY[s2], accY, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = (l >> 4) * 4 + i;        // D row held by this lane
+                        const int gi = x_half ? row : row - GRP;  // group instance
+                        if (gi < r) {
+                            float* dst = s_part + (w * CH + s_rowid[w][gi]) * RSL;
+                            if (x_half) {
+#pragma unroll
+                                for (int xb = 0; xb < NXB; ++xb)
+                                    if (xslot[xb] >= 0) dst[xslot[xb]] = accX[xb][i];
+                            } else if (yslot >= 0) {
+                                dst[yslot] = accY[i];
+                            }
+                        }
+                    }
+                    wave_lds_sync();
+                    r = 0;
+                }
+            }
+            __syncthreads();
+            // fixed-order sum of the four wave partials, moments -> mean2D / conic grads, one row
+            // per instance, re-zero the partials
+            const int jn = min(CH, cnt - c * CH);
+            constexpr int NC4 = RSL / 4;  // float4 columns; column pair 0|1 holds the moments
+            for (int it = t; it < jn * (NC4 - 1); it += kBlock) {
+                const int jj = it / (NC4 - 1);
+                const int col = it - jj * (NC4 - 1) + 1;  // 1 -> columns 0 and 1, else column col
+                const int j = c * CH + jj;
+                float4* row = reinterpret_cast<float4*>(a.rows + (size_t)s_slot[j] * RS);
+                if (col == 1) {
+                    float4 u0 = make_float4(0.f, 0.f, 0.f, 0.f), u1 = u0;
+#pragma unroll
+                    for (int ww = 0; ww < 4; ++ww) {
+                        float4* src = s_part4 + (ww * CH + jj) * NC4;
+                        const float4 v0 = src[0], v1 = src[1];
+                        u0.x += v0.x; u0.y += v0.y; u0.z += v0.z; u0.w += v0.w;
+                        u1.x += v1.x; u1.y += v1.y; u1.z += v1.z; u1.w += v1.w;
+                        src[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        src[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                    const float2 xy = s_xy[j];
+                    const float4 co = s_co[j];
+                    // slots: 0 Sx, 1 Sy, 2 depth, 3 Sxx, 4 Sxy, 5 Syy, 6 S0 (= opacity grad), 7 colour r
+                    const float S0 = u1.z, Sx = u0.x, Sy = u0.y, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
+                    const float d0x = xy.x - ctx, d0y = xy.y - cty;
+                    const float Sdx = d0x * S0 - Sx, Sdy = d0y * S0 - Sy;
+                    const float Sdxdx = d0x * d0x * S0 - 2.f * d0x * Sx + Sxx;
+                    const float Sdxdy = d0x * d0y * S0 - d0x * Sy - d0y * Sx + Sxy;
+                    const float Sdydy = d0y * d0y * S0 - 2.f * d0y * Sy + Syy;
+                    row[0] = make_float4(-0.5f * a.W * co.w * (co.x * Sdx + co.y * Sdy),
+                                         -0.5f * a.H * co.w * (co.z * Sdy + co.y * Sdx), u0.z, -0.5f * co.w * Sdxdx);
+                    row[1] = make_float4(-0.5f * co.w * Sdxdy, -0.5f * co.w * Sdydy, S0, u1.w);
+                } else {
+                    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int ww = 0; ww < 4; ++ww) {
+                        float4* src = s_part4 + (ww * CH + jj) * NC4 + col;
+                        const float4 v0 = *src;
+                        u.x += v0.x; u.y += v0.y; u.z += v0.z; u.w += v0.w;
+                        *src = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                    if (4 * col < RS) row[col] = u;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 template <int SMAX>
 static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL((render_bwd_kernel<SMAX>), dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0, stream, a);
+    const char* e = getenv("R3DG_BWD");  // "dpp" selects the DPP-reduction variant (A/B and cross-check)
+    const bool use_dpp = e && e[0] == 'd';
+    if (use_dpp)
+        hipLaunchKernelGGL((render_bwd_dpp_kernel<SMAX>), dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0, stream,
+                           a);
+    else
+        hipLaunchKernelGGL((render_bwd_mfma_kernel<SMAX>), dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0,
+                           stream, a);
     return hipGetLastError();
 }
 

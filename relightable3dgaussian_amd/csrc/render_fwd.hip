@@ -6,10 +6,12 @@
 //   * each batch of 256 sorted instances is staged in LDS once: xy, conic|opacity, and an AoS
 //     attribute row (colour, depth, [shader colour], features) read with ds_read_b128
 //     broadcasts -- the reference re-reads colours and features from HBM per pixel;
-//   * a conservative per-quadrant footprint mask (alpha >= 1/255 ellipse, widened) lets a
-//     wave skip an instance with one scalar branch. Skipping is exact: a skipped instance
-//     would have failed the reference's alpha test on every pixel of the quadrant
-//     (tests/test_gpu_parity.py checks cull on == cull off bit for bit);
+//   * a conservative per-quadrant footprint mask (alpha >= 1/255 ellipse, widened) decides
+//     which instances a wave visits. Skipping is exact: a skipped instance would have failed
+//     the reference's alpha test on every pixel of the quadrant (tests/test_gpu_parity.py
+//     checks cull on == cull off bit for bit). The masks are compacted at staging time into
+//     per-wave 32-bit chunk masks (one ballot per wave), so a wave iterates only its live
+//     instances with s_ff1 -- no per-instance scalar test;
 //   * early exit per wave (ballot) and per block (__syncthreads_count), as the reference;
 //   * XCD-aware tile order (r3dg_kernels.h).
 #include "r3dg_common.h"
@@ -46,8 +48,8 @@ __global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
     constexpr int NA4 = (FO + SMAX + 3) / 4;           // float4 per attribute row
     __shared__ float2 s_xy[kBlock];
     __shared__ float4 s_co[kBlock];
-    __shared__ uint32_t s_mask[kBlock];
     __shared__ float4 s_attr[kBlock * NA4];
+    __shared__ uint32_t s_bits[8][4];                  // [32-instance chunk][wave]: live-instance masks
 
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
     if (tile >= a.num_tiles) return;
@@ -70,13 +72,14 @@ __global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
 
     for (int base = 0; base < n; base += kBlock) {
         if (__syncthreads_count(done) == kBlock) break;
+        uint32_t m = 0;
         if (base + t < n) {
             const uint32_t gid = a.point_list[range.x + base + t];
             const float2 xy = a.means2D[gid];
             const float4 co = a.conic_opacity[gid];
             s_xy[t] = xy;
             s_co[t] = co;
-            s_mask[t] = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
+            m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
             float v[NA4 * 4];
 #pragma unroll
             for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
@@ -97,12 +100,22 @@ __global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
             for (int q = 0; q < NA4; ++q)
                 s_attr[t * NA4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
         }
+        // compaction: this wave's 64 staged slots are chunks 2w and 2w+1; one ballot per target wave
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const unsigned long long bal = __ballot((m >> b) & 1u);
+            if (l == 0) {
+                s_bits[2 * w][b] = (uint32_t)bal;
+                s_bits[2 * w + 1][b] = (uint32_t)(bal >> 32);
+            }
+        }
         __syncthreads();
-        const int cnt = min(kBlock, n - base);
-        if (__ballot(!done) != 0ull) {
-            for (int j = 0; j < cnt; ++j) {
-                const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
-                if (!((m >> w) & 1u)) continue;
+        bool alive = __ballot(!done) != 0ull;
+        for (int c = 0; c < 8 && alive; ++c) {
+            uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[c][w]);
+            while (bits) {
+                const int j = c * 32 + __builtin_ctz(bits);
+                bits &= bits - 1;
                 if (!done) {
                     const float2 xy = s_xy[j];
                     const float4 co = s_co[j];
@@ -131,7 +144,7 @@ __global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
                                     CS[2] += v[6] * wgt;
                                 }
 #pragma unroll
-                                for (int c = 0; c < SMAX; ++c) F[c] += v[FO + c] * wgt;
+                                for (int c2 = 0; c2 < SMAX; ++c2) F[c2] += v[FO + c2] * wgt;
                                 Dp += v[3] * wgt;
                                 Op += wgt;
                                 T = test_T;
@@ -140,7 +153,10 @@ __global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
                         }
                     }
                 }
-                if (__ballot(!done) == 0ull) break;
+                if (__ballot(!done) == 0ull) {  // converged here: a uniform exit
+                    alive = false;
+                    break;
+                }
             }
         }
     }

@@ -415,3 +415,19 @@ def test_autograd_wrapper(hip_ext):
     assert_close("scales.grad", scales.grad.cpu().numpy(), go["dL_dscales"], _grad_tol(go["dL_dscales"]), 2e-3)
     assert_close("rotations.grad", rots.grad.cpu().numpy(), go["dL_drotations"], _grad_tol(go["dL_drotations"]),
                  2e-3)
+
+
+@pytest.mark.parametrize("S", [11, 21])
+def test_backward_mfma_matches_dpp_variant(hip_ext, S):
+    """The MFMA reduction (default) and the DPP wave-reduction variant of the backward blend agree."""
+    scene, cam = synthetic.small_scene(P=3000, S=21, seed=40 + S, width=96, height=80)
+    h = hip_forward(hip_ext, scene, cam, S=S)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, S)
+    gm = hip_backward(hip_ext, h, dc, do, dd, df)
+    os.environ["R3DG_BWD"] = "dpp"
+    try:
+        gd = hip_backward(hip_ext, h, dc, do, dd, df)
+    finally:
+        del os.environ["R3DG_BWD"]
+    for k in gm:
+        assert_close(k, gm[k], gd[k], 1e-5 * max(float(np.abs(gd[k]).max()) if gd[k].size else 0.0, 1e-12), 1e-3)
