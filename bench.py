@@ -43,17 +43,6 @@ def algorithmic_bytes(L: int, npix: int, tiles: int, S: int) -> tuple[int, int]:
     return fwd, bwd
 
 
-def rank_camera(rank: int, world: int):
-    from relightable3dgaussian_amd import synthetic
-
-    cam = synthetic.m1_camera(W_M1, H_M1)
-    if world == 1:
-        return cam
-    yaw = math.radians((rank - (world - 1) / 2.0) * 1.0)  # small per-rank yaw: similar cost per view
-    R = np.array([[math.cos(yaw), 0, math.sin(yaw)], [0, 1, 0], [-math.sin(yaw), 0, math.cos(yaw)]])
-    return synthetic.make_camera(R, np.zeros(3), cam.fovx, cam.fovy, W_M1, H_M1)
-
-
 def load_traffic() -> dict | None:
     path = os.path.join(ROOT, "profiles", "traffic_latest.json")
     if not os.path.exists(path):
@@ -112,7 +101,9 @@ def main() -> None:
     from relightable3dgaussian_amd import synthetic
 
     _C = r3._C
-    cam = rank_camera(rank, world)
+    from relightable3dgaussian_amd import view_parallel
+
+    cam = view_parallel.rank_camera(synthetic.m1_camera(W_M1, H_M1), rank, world)
     scene = synthetic.m1_scene(P=args.P, S=S_M1, seed=0, cam=synthetic.m1_camera(W_M1, H_M1))
     t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32, device=dev)  # noqa: E731
     means3D, feats, opac = t(scene.means3D), t(scene.features), t(scene.opacity)
@@ -136,10 +127,7 @@ def main() -> None:
                                                 proj, cam.tanfovx, cam.tanfovy, g_color, g_opac, g_depth, g_feat,
                                                 sh, 3, campos, geom, L, binning, img, True, False)
         if world > 1:
-            # grads: means2D, colors, opacity, means3D, features, cov3D, sh, scales, rotations
-            flat = torch.cat([grads[3].reshape(-1), grads[6].reshape(-1), grads[2].reshape(-1),
-                              grads[7].reshape(-1), grads[8].reshape(-1), grads[4].reshape(-1)])
-            dist.all_reduce(flat)
+            view_parallel.all_reduce_grads(grads)
         return L
 
     for _ in range(args.warmup):
