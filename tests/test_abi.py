@@ -161,3 +161,15 @@ def test_product_package_never_imports_oracle():
                 bad = re.findall(r"^\s*(?:import oracle|from oracle|#include [\"<].*oracle.*)|libr3dg_oracle", text,
                                  flags=re.M)
                 assert not bad, (f, bad)
+
+
+def test_integration_shim_package():
+    """integration/r3dg_rasterization is importable under the reference's package name."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "integration")]))
+    code = ("from r3dg_rasterization import _C, GaussianRasterizer, RenderEquation; "
+            "import relightable3dgaussian_amd as r; assert _C is r._C; print('ok')")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]

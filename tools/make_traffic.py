@@ -1,0 +1,28 @@
+"""profiles/traffic_latest.json from a PMC pass summary (tools/pmc_summary.py output).
+
+HBM bytes per launch = FETCH_SIZE * 2 + WRITE_SIZE (KiB -> bytes), following
+MI355X_MICROARCH.md's gfx950 note (FETCH_SIZE reports half the bytes of wide reads; WRITE_SIZE is
+exact). The blend kernels' reads are mostly narrow gathers, for which the guide calls the
+correction uncalibrated: treat the absolute as an estimate, ratios between versions as exact."""
+import json
+import sys
+
+src, dst, config = sys.argv[1], sys.argv[2], sys.argv[3]
+d = json.load(open(src))
+
+
+def pick(prefix):
+    for k, v in d.items():
+        if k.startswith(prefix):
+            return k, v
+    raise KeyError(prefix)
+
+
+out = {"config": config, "source": src, "method": "FETCH_SIZE*2 + WRITE_SIZE (KiB*1024), mean per launch"}
+for name, prefix in [("render_fwd", "render_fwd_kernel"), ("render_bwd", "render_bwd_mfma_kernel"),
+                     ("gather_bwd", "gather_bwd_kernel"), ("preprocess", "preprocess_kernel")]:
+    k, v = pick(prefix)
+    out[name + "_kernel"] = k
+    out[name + "_bytes"] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))
+json.dump(out, open(dst, "w"), indent=1)
+print(json.dumps(out, indent=1))
