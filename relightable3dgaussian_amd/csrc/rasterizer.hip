@@ -306,6 +306,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     R3DG_REQUIRE(((g->scales && g->rotations) != (g->cov3D_precomp != nullptr)) || P == 0,
                  "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
     R3DG_REQUIRE(S == 0 || P == 0 || g->features, "rasterize_gaussians: features missing");
+    R3DG_REQUIRE(!g->sh || P == 0 || (s->D >= 0 && s->D <= 3 && (s->D + 1) * (s->D + 1) <= s->M && s->M <= 16),
+                 "rasterize_gaussians: SH degree must be 0..3 with (degree+1)^2 <= M <= 16 coefficients");
     R3DG_REQUIRE((long long)H * W * (S > 3 ? S : 3) < (1ll << 31), "rasterize_gaussians: image too large");
     *num_rendered = 0;
 
@@ -462,6 +464,8 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     R3DG_REQUIRE(s && g && gr && out, "rasterize_gaussians_backward: null argument");
     const int P = s->P, S = s->S, H = s->H, W = s->W, L = num_rendered;
     R3DG_REQUIRE(P >= 0 && L >= 0 && S >= 0 && S <= kMaxFeatures, "rasterize_gaussians_backward: invalid sizes");
+    R3DG_REQUIRE(!g->sh || P == 0 || (s->D >= 0 && s->D <= 3 && (s->D + 1) * (s->D + 1) <= s->M && s->M <= 16),
+                 "rasterize_gaussians_backward: SH degree must be 0..3 with (degree+1)^2 <= M <= 16 coefficients");
     if (P == 0) return R3DG_OK;
     const int gx = (W + kTileX - 1) / kTileX, gy = (H + kTileY - 1) / kTileY;
     const int T = gx * gy;

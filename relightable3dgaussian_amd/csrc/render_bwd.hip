@@ -598,10 +598,6 @@ __device__ static void sh_backward(int deg, int M, float3 pos, const float* camp
     b[9] = SH_C3_0 * y * (3.f * xx - yy); b[10] = SH_C3_1 * xy * z; b[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
     b[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy); b[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
     b[14] = SH_C3_5 * z * (xx - yy); b[15] = SH_C3_6 * x * (xx - 3.f * yy);
-    const int ncoef = deg > 2 ? 16 : (deg > 1 ? 9 : (deg > 0 ? 4 : 1));
-    for (int i = 0; i < M; ++i)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) dsh[3 * i + c] = i < ncoef ? b[i] * dRGB[c] : 0.f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         if (deg > 0) {
@@ -631,6 +627,11 @@ __device__ static void sh_backward(int deg, int M, float3 pos, const float* camp
             }
         }
     }
+    // dsh may alias sh (the gather kernel updates its LDS copy in place): written after the reads
+    const int ncoef = deg > 2 ? 16 : (deg > 1 ? 9 : (deg > 0 ? 4 : 1));
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dsh[3 * i + c] = i < ncoef ? b[i] * dRGB[c] : 0.f;
     const float dvx = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
     const float dvy = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
     const float dvz = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
@@ -678,28 +679,11 @@ __device__ static void cov3d_backward(float3 sc, float mod, float4 q, const floa
               4 * z * (E[1][1] + E[0][0]);
 }
 
+// Per-Gaussian part of the gather: writes the summed instance gradients, then computeCov2DCUDA,
+// the projection and SH backward (preprocessCUDA bwd) and computeCov3D backward. `s` holds the
+// summed row, `shl` this Gaussian's SH coefficients in LDS, replaced by dL/dsh on return.
 template <int SMAX>
-__global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
-    constexpr int NR = kRowFeat + SMAX;
-    constexpr int NQ = (NR + 3) / 4;
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= a.P) return;
-    const uint32_t start = g == 0 ? 0u : a.offsets[g - 1];
-    const uint32_t end = a.radii[g] > 0 ? a.offsets[g] : start;
-    float s[NQ * 4];
-#pragma unroll
-    for (int i = 0; i < NQ * 4; ++i) s[i] = 0.f;
-    const int RS = a.RS;
-    for (uint32_t k = start; k < end; ++k) {
-        const float4* row = reinterpret_cast<const float4*>(a.rows + (size_t)k * RS);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            if (4 * q < RS) {
-                const float4 v = row[q];
-                s[4 * q] += v.x; s[4 * q + 1] += v.y; s[4 * q + 2] += v.z; s[4 * q + 3] += v.w;
-            }
-        }
-    }
+__device__ __forceinline__ void gather_gaussian(const GatherBwdArgs& a, int g, const float* s, float* shl) {
     a.dL_dmeans2D[3 * g + 0] = s[kRowMean + 0];
     a.dL_dmeans2D[3 * g + 1] = s[kRowMean + 1];
     a.dL_dmeans2D[3 * g + 2] = s[kRowMean + 2];
@@ -716,8 +700,7 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     if (!(a.radii[g] > 0)) {
         dmean3[0] = dmean3[1] = dmean3[2] = 0.f;
         for (int i = 0; i < 6; ++i) dcov[i] = 0.f;
-        if (a.dL_dsh)
-            for (int i = 0; i < 3 * a.M; ++i) a.dL_dsh[(size_t)g * a.M * 3 + i] = 0.f;
+        for (int i = 0; i < 3 * a.M; ++i) shl[i] = 0.f;
         for (int i = 0; i < 3; ++i) a.dL_dscales[3 * g + i] = 0.f;
         for (int i = 0; i < 4; ++i) a.dL_drotations[4 * g + i] = 0.f;
         return;
@@ -804,7 +787,9 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
         const uint8_t cl = a.clamped[g];
         const float dRGB[3] = {s[kRowColor + 0] * ((cl & 1) ? 0.f : 1.f), s[kRowColor + 1] * ((cl & 2) ? 0.f : 1.f),
                                s[kRowColor + 2] * ((cl & 4) ? 0.f : 1.f)};
-        sh_backward(a.D, a.M, mean, a.campos, a.sh + (size_t)g * a.M * 3, dRGB, dm, a.dL_dsh + (size_t)g * a.M * 3);
+        sh_backward(a.D, a.M, mean, a.campos, shl, dRGB, dm, shl);
+    } else {
+        for (int i = 0; i < 3 * a.M; ++i) shl[i] = 0.f;
     }
     dmean3[0] = dm[0];
     dmean3[1] = dm[1];
@@ -817,6 +802,80 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     } else {
         for (int i = 0; i < 3; ++i) a.dL_dscales[3 * g + i] = 0.f;
         for (int i = 0; i < 4; ++i) a.dL_drotations[4 * g + i] = 0.f;
+    }
+}
+
+template <int SMAX>
+__global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
+    constexpr int NR = kRowFeat + SMAX;
+    constexpr int NQ = (NR + 3) / 4;       // float4 columns of a gradient row (upper bound)
+    constexpr int LPG = NQ <= 8 ? 8 : 16;  // lanes per Gaussian in the row-sum phase
+    constexpr int SHS = 49;                // LDS stride of one Gaussian's SH block (<= 48 used, odd)
+    constexpr int SUMF = 256 * NQ * 4, SHF = 256 * SHS;
+    __shared__ float4 s_buf4[((SUMF > SHF ? SUMF : SHF) + 3) / 4];
+    float* s_buf = reinterpret_cast<float*>(s_buf4);
+    const int t = threadIdx.x;
+    const int g0 = blockIdx.x * 256;
+    const int nq = a.RS / 4;
+
+    // ---- phase 1: per-Gaussian sums of its contiguous rows. LPG lanes per Gaussian, lane c owns
+    // float4 column c, so a row is read as one contiguous 16*nq-byte segment. Rows are added in
+    // slot order, the same fixed order for every run.
+    {
+        const int c = t % LPG, gl0 = t / LPG;
+        const float4* col = reinterpret_cast<const float4*>(a.rows) + c;
+        for (int r = 0; r < LPG; ++r) {
+            const int gl = r * (256 / LPG) + gl0;
+            const int g = g0 + gl;
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (g < a.P && c < nq && a.radii[g] > 0) {
+                uint32_t k = g == 0 ? 0u : a.offsets[g - 1];
+                const uint32_t end = a.offsets[g];
+                for (; k + 4 <= end; k += 4) {
+                    const float4 v0 = col[(size_t)k * nq], v1 = col[(size_t)(k + 1) * nq];
+                    const float4 v2 = col[(size_t)(k + 2) * nq], v3 = col[(size_t)(k + 3) * nq];
+                    acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
+                    acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
+                    acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
+                    acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
+                }
+                for (; k < end; ++k) {
+                    const float4 v = col[(size_t)k * nq];
+                    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+                }
+            }
+            if (c < NQ) s_buf4[gl * NQ + c] = acc;
+        }
+    }
+    __syncthreads();
+    const int g = g0 + t;
+    float s[NQ * 4];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const float4 v = s_buf4[t * NQ + q];
+        s[4 * q] = v.x; s[4 * q + 1] = v.y; s[4 * q + 2] = v.z; s[4 * q + 3] = v.w;
+    }
+    __syncthreads();
+    // ---- SH coefficients of the block's Gaussians: one coalesced copy into LDS ----
+    const int M3 = 3 * a.M;
+    const int ng = min(256, a.P - g0);
+    float* shl = s_buf + t * SHS;
+    if (a.sh && a.dL_dsh) {
+        const float* src = a.sh + (size_t)g0 * M3;
+        for (int f = t; f < ng * M3; f += 256) {
+            const int gg = f / M3;
+            s_buf[gg * SHS + (f - gg * M3)] = src[f];
+        }
+    }
+    __syncthreads();
+    if (g < a.P) gather_gaussian<SMAX>(a, g, s, shl);
+    __syncthreads();
+    if (a.dL_dsh) {
+        float* dst = a.dL_dsh + (size_t)g0 * M3;
+        for (int f = t; f < ng * M3; f += 256) {
+            const int gg = f / M3;
+            dst[f] = s_buf[gg * SHS + (f - gg * M3)];
+        }
     }
 }
 
