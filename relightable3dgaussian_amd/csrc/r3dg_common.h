@@ -134,7 +134,6 @@ __device__ __forceinline__ float4 xform_point4x4(float3 p, const float* m) {
 }
 
 // Wave-wide sum over 64 lanes with DPP (result valid in lane 63).
-__device__ __forceinline__ float dpp_f(float v, int ctrl_dummy);
 
 template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF, bool BOUND = false>
 __device__ __forceinline__ float dpp_mov(float v) {
@@ -153,5 +152,14 @@ __device__ __forceinline__ float wave_sum_to_lane63(float v) {
 }
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Exponent of the 2D Gaussian at offset (dx, dy) from its centre: -0.5 (a dx^2 + c dy^2) - b dx dy
+// (forward.cu:478, backward.cu:530). One fixed FMA pattern, so every call site -- forward and
+// backward, first or second instance of an unrolled pair -- rounds identically.
+__device__ __forceinline__ float gauss_power(float4 co, float dx, float dy) {
+#pragma clang fp contract(off)
+    const float q = __builtin_fmaf(co.x * dx, dx, (co.z * dy) * dy);
+    return __builtin_fmaf(-0.5f, q, -((co.y * dx) * dy));
+}
 
 }  // namespace r3dg

@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
                     co = s_co[j];
                     dx = xy.x - pfx;
                     dy = xy.y - pfy;
-                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    const float power = gauss_power(co, dx, dy);
                     if (power > 0.0f) {
                         contrib = false;
                     } else {
@@ -313,7 +313,10 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
     // ---- B operands: X[pixel][channel] and Y[pixel][moment] for k-step s (pixel 4s + (l>>4)) ----
     float* wq = s_wq[w];
     float bX[NXB][16];
-    float bY[16];
+    // Y[pixel][moment] = [1, x, y, x^2, xy, y^2][nch] at pixel 4*s2 + (l>>4) of this wave: its x
+    // offset depends only on s2&1 and its y offset is wave-uniform per s2, so the B operand of k-step
+    // s2 is yA[s2&1] + y*(yB[s2&1] + y*yC) (exact: every term but one is a zero product).
+    float yA[2], yB[2], yC;
     {
 #pragma unroll
         for (int xb = 0; xb < NXB; ++xb) {
@@ -333,19 +336,12 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
         }
         const int nch = l & 15;
 #pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) {
-            const int pl = 4 * s2 + (l >> 4);  // pixel lane of k-step s2
-            const float xo = (float)((w & 1) * 8 + (pl & 7)) - 7.5f;
-            const float yo = (float)((w >> 1) * 8 + (pl >> 3)) - 7.5f;
-            float v = 0.f;
-            v = nch == 0 ? 1.f : v;
-            v = nch == 1 ? xo : v;
-            v = nch == 2 ? yo : v;
-            v = nch == 3 ? xo * xo : v;
-            v = nch == 4 ? xo * yo : v;
-            v = nch == 5 ? yo * yo : v;
-            bY[s2] = v;
+        for (int h = 0; h < 2; ++h) {
+            const float xo = (float)((w & 1) * 8 + 4 * h + (l >> 4)) - 7.5f;
+            yA[h] = nch == 0 ? 1.f : (nch == 1 ? xo : (nch == 3 ? xo * xo : 0.f));
+            yB[h] = nch == 2 ? 1.f : (nch == 4 ? xo : 0.f);
         }
+        yC = nch == 5 ? 1.f : 0.f;
     }
 
     // The reference keeps one accum_rec per channel (colour, features, depth); all share the same
@@ -426,50 +422,64 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
             if (lo >= CH) bits = 0;
             else if (lo > 0) bits &= ~0u << lo;
             int r = 0;  // rows filled in the current MFMA group
-            while (bits) {
-                const int jj = __builtin_ctz(bits);
-                bits &= bits - 1;
-                const int j = c * CH + jj;
-                const int p = hi - 1 - j;  // position in the tile range (reference `contributor`)
-                float wv = 0.f, qv = 0.f;
-                if (inside && p < last) {
-                    const float2 xy = s_xy[j];
-                    const float4 co = s_co[j];
-                    const float dx = xy.x - pfx, dy = xy.y - pfy;
-                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                    if (!(power > 0.0f)) {
-                        const float G = __expf(power);
-                        const float alpha = fminf(0.99f, co.w * G);
-                        if (!(alpha < 1.0f / 255.0f)) {
-                            const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
-                            T = T * rinv;
-                            const float dchannel_dcolor = alpha * T;
-                            float v[NA4 * 4];
+            // One blend step of the reference's per-pixel loop (backward.cu:520-611), predicated
+            // rather than branched: every LDS read is issued up front and a non-contributing pixel
+            // (outside, past n_contrib, power > 0 or alpha < 1/255) leaves its state unchanged.
+            auto step = [&](int j, bool live, float& wv, float& qv) {
+#pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
+                const float2 xy = s_xy[j];
+                const float4 co = s_co[j];
+                float v[NA4 * 4];
 #pragma unroll
-                            for (int q = 0; q < NA4; ++q) {
-                                const float4 rr = s_attr[j * NA4 + q];
-                                v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
-                            }
-                            float dot = v[0] * g[0] + v[1] * g[1] + v[2] * g[2] + v[3] * gd;
-#pragma unroll
-                            for (int c2 = 0; c2 < SMAX; ++c2) dot += v[4 + c2] * gf[c2];
-                            acc_dot = last_alpha * last_dot + (1.f - last_alpha) * acc_dot;
-                            last_dot = dot;
-                            float dL_dalpha = dot - acc_dot;
-                            acc_o = last_alpha + (1.f - last_alpha) * acc_o;
-                            dL_dalpha += (1.0f - acc_o) * go;
-                            dL_dalpha *= T;
-                            last_alpha = alpha;
-                            dL_dalpha += (-T_final * rinv) * bg_dot;
-                            wv = dchannel_dcolor;
-                            qv = G * dL_dalpha;
-                        }
-                    }
+                for (int q = 0; q < NA4; ++q) {
+                    const float4 rr = s_attr[j * NA4 + q];
+                    v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
                 }
-                wq[r * WQS + l] = wv;
-                wq[(GRP + r) * WQS + l] = qv;
-                if (l == 0) s_rowid[w][r] = jj;
-                ++r;
+                const int p = hi - 1 - j;  // position in the tile range (reference `contributor`)
+                const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
+                const float G = __expf(power);
+                const float alpha = fminf(0.99f, co.w * G);
+                const bool ok = live && inside && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
+                const float Tn = T * rinv;
+                float dot = v[0] * g[0];
+                dot = __builtin_fmaf(v[1], g[1], dot);
+                dot = __builtin_fmaf(v[2], g[2], dot);
+                dot = __builtin_fmaf(v[3], gd, dot);
+#pragma unroll
+                for (int c2 = 0; c2 < SMAX; ++c2) dot = __builtin_fmaf(v[4 + c2], gf[c2], dot);
+                const float acc_dot_n = __builtin_fmaf(last_alpha, last_dot, (1.f - last_alpha) * acc_dot);
+                const float acc_o_n = __builtin_fmaf(1.f - last_alpha, acc_o, last_alpha);
+                float dL_dalpha = __builtin_fmaf(1.0f - acc_o_n, go, dot - acc_dot_n);
+                dL_dalpha = __builtin_fmaf(dL_dalpha, Tn, (-T_final * rinv) * bg_dot);
+                wv = ok ? alpha * Tn : 0.f;
+                qv = ok ? G * dL_dalpha : 0.f;
+                T = ok ? Tn : T;
+                acc_dot = ok ? acc_dot_n : acc_dot;
+                last_dot = ok ? dot : last_dot;
+                acc_o = ok ? acc_o_n : acc_o;
+                last_alpha = ok ? alpha : last_alpha;
+            };
+            while (bits) {
+                // two compacted instances per iteration: the second one's LDS reads and exp
+                // overlap the first one's dependent chain
+                const int jj0 = __builtin_ctz(bits);
+                bits &= bits - 1;
+                const bool has1 = bits != 0u;
+                const int jj1 = has1 ? __builtin_ctz(bits) : jj0;
+                bits &= bits - 1;
+                float wv0, qv0, wv1, qv1;
+                step(c * CH + jj0, true, wv0, qv0);
+                step(c * CH + jj1, has1, wv1, qv1);
+                wq[r * WQS + l] = wv0;
+                wq[(GRP + r) * WQS + l] = qv0;
+                wq[(r + 1) * WQS + l] = wv1;
+                wq[(GRP + r + 1) * WQS + l] = qv1;
+                if (l == 0) {
+                    s_rowid[w][r] = jj0;
+                    s_rowid[w][r + 1] = jj1;
+                }
+                r += has1 ? 2 : 1;
                 if (r == GRP || bits == 0) {
                     // [8 w rows | 8 q rows] x [64 px] against X (16 ch) and Y (moments): rows 0..7
                     // of w.X and rows 8..15 of q.Y are the useful halves
@@ -483,7 +493,9 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
 #pragma unroll
                         for (int xb = 0; xb < NXB; ++xb)
                             accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
-                        accY = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bY[s2], accY, 0, 0, 0);
+                        const float yo = (float)((w >> 1) * 8 + (s2 >> 1)) - 7.5f;
+                        const float by = yA[s2 & 1] + yo * (yB[s2 & 1] + yo * yC);
+                        accY = __builtin_amdgcn_mfma_f32_16x16x4f32(av, by, accY, 0, 0, 0);
                     }
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {

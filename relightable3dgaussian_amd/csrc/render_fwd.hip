@@ -110,49 +110,54 @@ __global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
             }
         }
         __syncthreads();
+        // One blend step of renderCUDA (forward.cu:470-520): the tests are predicated, every LDS
+        // read of the instance is issued before them, and only the accumulation is a branch.
+        auto step = [&](int j, bool live) {
+#pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
+            const float2 xy = s_xy[j];
+            const float4 co = s_co[j];
+            float v[NA4 * 4];
+#pragma unroll
+            for (int q = 0; q < NA4; ++q) {
+                const float4 r = s_attr[j * NA4 + q];
+                v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
+            }
+            const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
+            const float alpha = fminf(0.99f, co.w * __expf(power));
+            const bool contrib = live && !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const float test_T = T * (1.0f - alpha);
+            const bool stop = test_T < 0.0001f;
+            done = done || (contrib && stop);
+            if (contrib && !stop) {
+                const float wgt = alpha * T;
+                C[0] = __builtin_fmaf(v[0], wgt, C[0]);
+                C[1] = __builtin_fmaf(v[1], wgt, C[1]);
+                C[2] = __builtin_fmaf(v[2], wgt, C[2]);
+                if constexpr (SHADER) {
+                    CS[0] = __builtin_fmaf(v[4], wgt, CS[0]);
+                    CS[1] = __builtin_fmaf(v[5], wgt, CS[1]);
+                    CS[2] = __builtin_fmaf(v[6], wgt, CS[2]);
+                }
+#pragma unroll
+                for (int c2 = 0; c2 < SMAX; ++c2) F[c2] = __builtin_fmaf(v[FO + c2], wgt, F[c2]);
+                Dp = __builtin_fmaf(v[3], wgt, Dp);
+                Op += wgt;
+                T = test_T;
+                last = (uint32_t)(base + j + 1);
+            }
+        };
         bool alive = __ballot(!done) != 0ull;
         for (int c = 0; c < 8 && alive; ++c) {
             uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[c][w]);
             while (bits) {
-                const int j = c * 32 + __builtin_ctz(bits);
+                // two compacted instances per iteration (the second one's reads overlap the first)
+                const int j0 = c * 32 + __builtin_ctz(bits);
                 bits &= bits - 1;
-                if (!done) {
-                    const float2 xy = s_xy[j];
-                    const float4 co = s_co[j];
-                    const float dx = xy.x - pfx, dy = xy.y - pfy;
-                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                    if (!(power > 0.0f)) {
-                        const float alpha = fminf(0.99f, co.w * __expf(power));
-                        if (!(alpha < 1.0f / 255.0f)) {
-                            const float test_T = T * (1.0f - alpha);
-                            if (test_T < 0.0001f) {
-                                done = true;
-                            } else {
-                                const float wgt = alpha * T;
-                                float v[NA4 * 4];
-#pragma unroll
-                                for (int q = 0; q < NA4; ++q) {
-                                    const float4 r = s_attr[j * NA4 + q];
-                                    v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
-                                }
-                                C[0] += v[0] * wgt;
-                                C[1] += v[1] * wgt;
-                                C[2] += v[2] * wgt;
-                                if constexpr (SHADER) {
-                                    CS[0] += v[4] * wgt;
-                                    CS[1] += v[5] * wgt;
-                                    CS[2] += v[6] * wgt;
-                                }
-#pragma unroll
-                                for (int c2 = 0; c2 < SMAX; ++c2) F[c2] += v[FO + c2] * wgt;
-                                Dp += v[3] * wgt;
-                                Op += wgt;
-                                T = test_T;
-                                last = (uint32_t)(base + j + 1);
-                            }
-                        }
-                    }
-                }
+                const bool has1 = bits != 0u;
+                const int j1 = has1 ? c * 32 + __builtin_ctz(bits) : j0;
+                bits &= bits - 1;
+                step(j0, true);
+                step(j1, has1);
                 if (__ballot(!done) == 0ull) {  // converged here: a uniform exit
                     alive = false;
                     break;
@@ -242,7 +247,7 @@ __global__ void __launch_bounds__(kBlock) intermediate_kernel(IntermediateArgs a
             const float2 xy = s_xy[j];
             const float4 co = s_co[j];
             const float dx = xy.x - (float)px, dy = xy.y - (float)py;
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            const float power = gauss_power(co, dx, dy);
             if (power > 0.0f) continue;
             const float G = __expf(power);
             const float alpha = fminf(0.99f, co.w * G);
