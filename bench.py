@@ -158,8 +158,10 @@ def main() -> None:
     value = world * npix * args.steps / elapsed / 1e6
     tiles = ((W + 15) // 16) * ((H + 15) // 16)
     bf, bb = algorithmic_bytes(L, npix, tiles, S_M1)
-    avg = {k: (v[1] / v[0] if v[0] else float("nan")) for k, v in prof.items()}
-    t_kern = (avg["render_fwd"] + avg["render_bwd"]) / 1e3
+    # per-step device time of each stage (sort = depth sort + tile sort: two scopes per step)
+    avg = {k: v[1] / args.steps for k, v in prof.items()}
+    launch = {k: (v[1] / v[0] if v[0] else float("nan")) for k, v in prof.items()}
+    t_kern = (launch["render_fwd"] + launch["render_bwd"]) / 1e3
     achieved = (bf + bb) / t_kern / 1e9
     traffic = None
     tr = load_traffic()

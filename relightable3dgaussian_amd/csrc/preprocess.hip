@@ -101,6 +101,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     if (idx >= a.P) return;
     a.radii[idx] = 0;
     a.tiles_touched[idx] = 0;
+    a.depth_keys[idx] = 0xffffffffu;
     const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     const float3 pv = xform_point4x3(p, a.view);
     if (pv.z <= 0.2f) {  // auxiliary.h:154 (the reference __trap()s when prefiltered; we flag it)
@@ -140,6 +141,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     a.means2D[idx] = make_float2(px, py);
     a.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, a.opacity[idx]);
     a.tiles_touched[idx] = (uint32_t)((y1 - y0) * (x1 - x0));
+    a.depth_keys[idx] = __float_as_uint(pv.z);
 }
 
 // rasterizer_impl.cu:56-68 (checkFrustum)
@@ -154,43 +156,64 @@ __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* _
 // rasterizer_impl.cu:72-113 (duplicateWithKeys). The value sorted alongside each key is its
 // unsorted slot, so the sort permutation can route backward contributions to Gaussian-
 // contiguous rows; gid_of_slot maps a slot back to its Gaussian.
-__global__ void __launch_bounds__(256) duplicate_keys_kernel(int P, const float2* __restrict__ means2D,
-                                                             const float* __restrict__ depths,
-                                                             const uint32_t* __restrict__ offsets,
-                                                             const int* __restrict__ radii, int grid_x, int grid_y,
-                                                             uint64_t* __restrict__ keys,
-                                                             uint32_t* __restrict__ gid_of_slot) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= P) return;
-    const int r = radii[idx];
-    if (r <= 0) return;
-    uint32_t off = idx == 0 ? 0u : offsets[idx - 1];
-    int x0, y0, x1, y1;
-    const float2 m = means2D[idx];
-    get_rect(m.x, m.y, r, grid_x, grid_y, x0, y0, x1, y1);
-    const uint64_t dbits = (uint64_t)__float_as_uint(depths[idx]);
-    for (int y = y0; y < y1; ++y)
-        for (int x = x0; x < x1; ++x) {
-            keys[off] = ((uint64_t)(uint32_t)(y * grid_x + x) << 32) | dbits;
-            gid_of_slot[off] = (uint32_t)idx;
-            ++off;
+// duplicateWithKeys (rasterizer_impl.cu:72-113) in depth order. Block b expands the Gaussians of
+// depth ranks [256b, 256b+256) (ascending depth bits, ties by ascending id) into their tiles,
+// row-major over each rect as the reference. Their instances occupy one contiguous range of the
+// depth-ordered list, so the block writes it cooperatively (coalesced): output position q finds
+// its Gaussian by binary search over the block's instance offsets. A stable sort of this list by
+// tile reproduces the reference's stable sort by (tile << 32 | depth bits) with a 13-bit key.
+__global__ void __launch_bounds__(256) duplicate_in_depth_order_kernel(
+    int P, const uint32_t* __restrict__ order, const uint32_t* __restrict__ depth_scan,
+    const float2* __restrict__ means2D, const int* __restrict__ radii, int grid_x, int grid_y,
+    uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ gid_out) {
+    __shared__ uint32_t s_end[256];  // inclusive end of each Gaussian's instances, block-relative
+    __shared__ uint32_t s_gid[256];
+    __shared__ int s_x0[256], s_y0[256], s_w[256];
+    const int t = threadIdx.x;
+    const int i0 = blockIdx.x * 256;
+    const int n = min(256, P - i0);
+    const uint32_t base = i0 == 0 ? 0u : depth_scan[i0 - 1];
+    if (t < n) {
+        const uint32_t g = order[i0 + t];
+        s_end[t] = depth_scan[i0 + t] - base;
+        s_gid[t] = g;
+        const int r = radii[g];
+        int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+        if (r > 0) {
+            const float2 m = means2D[g];
+            get_rect(m.x, m.y, r, grid_x, grid_y, x0, y0, x1, y1);
         }
+        s_x0[t] = x0;
+        s_y0[t] = y0;
+        s_w[t] = max(x1 - x0, 1);
+    }
+    __syncthreads();
+    const uint32_t total = s_end[n - 1];
+    for (uint32_t q = t; q < total; q += 256) {
+        int lo = 0, hi = n - 1;  // first Gaussian whose end > q
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_end[mid] > q) hi = mid;
+            else lo = mid + 1;
+        }
+        const uint32_t k = q - (lo == 0 ? 0u : s_end[lo - 1]);
+        const int w = s_w[lo];
+        const int x = s_x0[lo] + (int)(k % (uint32_t)w), y = s_y0[lo] + (int)(k / (uint32_t)w);
+        tile_keys[base + q] = (uint32_t)(y * grid_x + x);
+        gid_out[base + q] = s_gid[lo];
+    }
 }
 
-// rasterizer_impl.cu:118-140 (identifyTileRanges), fused with the gather of sorted Gaussian ids.
-__global__ void __launch_bounds__(256) identify_ranges_kernel(int L, const uint64_t* __restrict__ keys,
-                                                              const uint32_t* __restrict__ sorted_slot,
-                                                              const uint32_t* __restrict__ gid_of_slot,
-                                                              uint32_t* __restrict__ point_list,
+// rasterizer_impl.cu:118-140 (identifyTileRanges)
+__global__ void __launch_bounds__(256) identify_ranges_kernel(int L, const uint32_t* __restrict__ tiles,
                                                               uint2* __restrict__ ranges) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= L) return;
-    point_list[idx] = gid_of_slot[sorted_slot[idx]];
-    const uint32_t cur = (uint32_t)(keys[idx] >> 32);
+    const uint32_t cur = tiles[idx];
     if (idx == 0) {
         ranges[cur].x = 0;
     } else {
-        const uint32_t prev = (uint32_t)(keys[idx - 1] >> 32);
+        const uint32_t prev = tiles[idx - 1];
         if (cur != prev) {
             ranges[prev].y = idx;
             ranges[cur].x = idx;

@@ -55,16 +55,33 @@ struct GeomState {
     float* stencil_opacity; // [P]
     uint8_t* clamped;       // [P] bit c: SH colour channel c clamped at 0
     uint32_t* tiles_touched;// [P]
-    uint32_t* point_offsets;// [P] inclusive scan of tiles_touched
+    uint32_t* point_offsets;// [P] inclusive scan of tiles_touched (Gaussian-contiguous slots)
+    uint32_t* depth_keys;   // [P] depth bits (0xffffffff: not visible)
+    uint32_t* depth_keys_sorted; // [P]
+    uint32_t* depth_order;  // [P] Gaussian ids by ascending depth (stable)
+    uint32_t* depth_scan;   // [P] inclusive scan of tiles_touched in depth order
     void* scan_temp;
     size_t scan_temp_bytes;
+    void* depth_sort_temp;
+    size_t depth_sort_temp_bytes;
+    void* depth_scan_temp;
+    size_t depth_scan_temp_bytes;
+};
+
+// tiles_touched of the i-th Gaussian in depth order (input of the depth-order scan)
+struct TouchedInDepthOrder {
+    const uint32_t* touched;
+    const uint32_t* order;
+    __host__ __device__ uint32_t operator()(uint32_t i) const { return touched[order[i]]; }
 };
 struct BinningState {
-    uint64_t* keys_unsorted;  // [L] tile << 32 | float bits(depth)
-    uint64_t* keys_sorted;    // [L]
-    uint32_t* gid_of_slot;    // [L] Gaussian id of each unsorted (Gaussian-contiguous) slot
-    uint32_t* sorted_slot;    // [L] unsorted slot of each sorted instance (the sort permutation)
-    uint32_t* point_list;     // [L] Gaussian ids in sorted order (reference point_list)
+    // Instances are generated in depth order (Gaussians sorted by depth bits), then stably sorted
+    // by tile: the result is the reference's stable sort by (tile << 32 | depth bits). The sort
+    // values are Gaussian ids, so the sorted values are the reference's point_list.
+    uint32_t* tile_keys;    // [L] tile of each instance, depth order (sort input)
+    uint32_t* tile_sorted;  // [L] tile of each sorted instance
+    uint32_t* gid_in;       // [L] Gaussian of each depth-ordered instance (sort values)
+    uint32_t* point_list;   // [L] Gaussian ids in sorted order (reference point_list)
     void* sort_temp;
     size_t sort_temp_bytes;
 };

@@ -21,6 +21,7 @@ struct PreprocessArgs {
     const float* campos;
     int* radii;
     uint32_t* tiles_touched;
+    uint32_t* depth_keys;  // float bits of the view depth, 0xffffffff when not visible
     float* depths;
     float2* means2D;
     float* cov3D;
@@ -59,7 +60,8 @@ __host__ __device__ inline int row_stride(int S) { return ((kRowFeat + S) + 3) &
 struct RenderBwdArgs {
     const uint2* ranges;
     const uint32_t* point_list;
-    const uint32_t* sorted_slot;
+    const uint32_t* offsets;   // inclusive scan of tiles touched: Gaussian g owns slots [offsets[g-1], offsets[g])
+    const int* radii;
     const float2* means2D;
     const float4* conic_opacity;
     const float* depths;
@@ -74,7 +76,7 @@ struct RenderBwdArgs {
     const float* dL_dpix_d;
     const float* dL_dpix_f;    // feature grads, layout gflay
     FeatureLayout gflay;
-    int S, W, H, grid_x, num_tiles, cull, backward_geometry, RS;
+    int S, W, H, grid_x, grid_y, num_tiles, cull, backward_geometry, RS;
     float* rows;               // [L, RS]
 };
 
@@ -132,11 +134,19 @@ struct IntermediateArgs {
 // kernels (defined in the .hip translation units)
 __global__ void preprocess_kernel(PreprocessArgs a);
 __global__ void mark_visible_kernel(int P, const float* means3D, const float* view, uint8_t* present);
-__global__ void duplicate_keys_kernel(int P, const float2* means2D, const float* depths, const uint32_t* offsets,
-                                      const int* radii, int grid_x, int grid_y, uint64_t* keys,
-                                      uint32_t* gid_of_slot);
-__global__ void identify_ranges_kernel(int L, const uint64_t* keys, const uint32_t* sorted_slot,
-                                       const uint32_t* gid_of_slot, uint32_t* point_list, uint2* ranges);
+__global__ void duplicate_in_depth_order_kernel(int P, const uint32_t* order, const uint32_t* depth_scan,
+                                                const float2* means2D, const int* radii, int grid_x, int grid_y,
+                                                uint32_t* tile_keys, uint32_t* gid_out);
+__global__ void identify_ranges_kernel(int L, const uint32_t* tiles, uint2* ranges);
+
+// Slot of the instance (Gaussian g, tile) in the reference's unsorted, Gaussian-contiguous order:
+// offsets[g-1] + row-major index of the tile in g's rect (duplicateWithKeys, rasterizer_impl.cu:92-107).
+__device__ __forceinline__ uint32_t instance_slot(const uint32_t* offsets, float2 xy, int radius, uint32_t g,
+                                                  int tx, int ty, int grid_x, int grid_y) {
+    int x0, y0, x1, y1;
+    get_rect(xy.x, xy.y, radius, grid_x, grid_y, x0, y0, x1, y1);
+    return (g == 0 ? 0u : offsets[g - 1]) + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
+}
 __global__ void xyz_normal_kernel(XyzNormalArgs a);
 __global__ void intermediate_kernel(IntermediateArgs a);
 

@@ -55,11 +55,35 @@ static size_t scan_temp_size(size_t P) {
     return bytes;
 }
 
-static size_t sort_temp_size(size_t L) {
+// Always the onesweep radix sort: rocprim's default switches to a merge sort below 2^20 items,
+// which is several times slower for the 1M-Gaussian depth sort.
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, 0>;
+
+static size_t sort_temp_size(size_t L) {  // tile sort of the instances
     size_t bytes = 0;
-    uint64_t* k = nullptr;
-    uint32_t* v = nullptr;
-    rocprim::radix_sort_pairs(nullptr, bytes, k, k, rocprim::counting_iterator<uint32_t>(0), v, L, 0, 64, 0);
+    uint32_t* k = nullptr;
+    rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, k, k, k, k, L, 0, 32, 0);
+    return bytes;
+}
+
+static size_t depth_sort_temp_size(size_t P) {  // depth sort of the Gaussians
+    size_t bytes = 0;
+    uint32_t* k = nullptr;
+    rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, k, k, rocprim::counting_iterator<uint32_t>(0), k, P, 0,
+                                          32, 0);
+    return bytes;
+}
+
+static auto depth_order_touched(const uint32_t* touched, const uint32_t* order) {
+    return rocprim::make_transform_iterator(rocprim::counting_iterator<uint32_t>(0),
+                                            TouchedInDepthOrder{touched, order});
+}
+
+static size_t depth_scan_temp_size(size_t P) {
+    size_t bytes = 0;
+    uint32_t* d = nullptr;
+    rocprim::inclusive_scan(nullptr, bytes, depth_order_touched(d, d), d, P, rocprim::plus<uint32_t>(), 0);
     return bytes;
 }
 
@@ -85,8 +109,16 @@ static GeomState carve_geom(uintptr_t p, size_t P, uintptr_t* end) {
     g.clamped = carve<uint8_t>(p, P);
     g.tiles_touched = carve<uint32_t>(p, P);
     g.point_offsets = carve<uint32_t>(p, P);
+    g.depth_keys = carve<uint32_t>(p, P);
+    g.depth_keys_sorted = carve<uint32_t>(p, P);
+    g.depth_order = carve<uint32_t>(p, P);
+    g.depth_scan = carve<uint32_t>(p, P);
     g.scan_temp_bytes = scan_temp_size(P);
     g.scan_temp = carve<char>(p, g.scan_temp_bytes);
+    g.depth_sort_temp_bytes = depth_sort_temp_size(P);
+    g.depth_sort_temp = carve<char>(p, g.depth_sort_temp_bytes);
+    g.depth_scan_temp_bytes = depth_scan_temp_size(P);
+    g.depth_scan_temp = carve<char>(p, g.depth_scan_temp_bytes);
     if (end) *end = p;
     return g;
 }
@@ -99,10 +131,9 @@ GeomState geom_state_from(void* base, size_t P) { return carve_geom((uintptr_t)b
 
 static BinningState carve_binning(uintptr_t p, size_t L, uintptr_t* end) {
     BinningState b{};
-    b.keys_unsorted = carve<uint64_t>(p, L);
-    b.keys_sorted = carve<uint64_t>(p, L);
-    b.gid_of_slot = carve<uint32_t>(p, L);
-    b.sorted_slot = carve<uint32_t>(p, L);
+    b.tile_keys = carve<uint32_t>(p, L);
+    b.tile_sorted = carve<uint32_t>(p, L);
+    b.gid_in = carve<uint32_t>(p, L);
     b.point_list = carve<uint32_t>(p, L);
     b.sort_temp_bytes = sort_temp_size(L);
     b.sort_temp = carve<char>(p, b.sort_temp_bytes);
@@ -347,7 +378,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         pa.means3D = g->means3D; pa.scales = g->scales; pa.rotations = g->rotations; pa.opacity = g->opacity;
         pa.sh = g->sh; pa.cov3D_precomp = g->cov3D_precomp; pa.colors_precomp = g->colors_precomp;
         pa.view = s->viewmatrix; pa.proj = s->projmatrix; pa.campos = s->campos;
-        pa.radii = radii; pa.tiles_touched = geom.tiles_touched; pa.depths = geom.depths;
+        pa.radii = radii; pa.tiles_touched = geom.tiles_touched; pa.depth_keys = geom.depth_keys;
+        pa.depths = geom.depths;
         pa.means2D = geom.means2D; pa.cov3D = geom.cov3D; pa.conic_opacity = geom.conic_opacity;
         pa.rgb = geom.rgb; pa.clamped = geom.clamped; pa.error_flag = nullptr;
         {
@@ -359,6 +391,19 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         size_t tb = geom.scan_temp_bytes;
         R3DG_CHECK_HIP(rocprim::inclusive_scan(geom.scan_temp, tb, geom.tiles_touched, geom.point_offsets,
                                                (size_t)P, rocprim::plus<uint32_t>(), st));
+        {
+            // Gaussians by ascending depth bits, stable (ties keep ascending id), then the
+            // instance offsets in that order; both overlap the host read of num_rendered below
+            ProfScope ps(R3DG_PROF_SORT, st);
+            size_t db = geom.depth_sort_temp_bytes;
+            R3DG_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(geom.depth_sort_temp, db, geom.depth_keys,
+                                                     geom.depth_keys_sorted, rocprim::counting_iterator<uint32_t>(0),
+                                                     geom.depth_order, (size_t)P, 0, 32, st));
+            size_t sb2 = geom.depth_scan_temp_bytes;
+            R3DG_CHECK_HIP(rocprim::inclusive_scan(geom.depth_scan_temp, sb2,
+                                                   depth_order_touched(geom.tiles_touched, geom.depth_order),
+                                                   geom.depth_scan, (size_t)P, rocprim::plus<uint32_t>(), st));
+        }
         uint32_t Lh = 0;
         R3DG_CHECK_HIP(hipMemcpyAsync(&Lh, geom.point_offsets + P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         R3DG_CHECK_HIP(hipStreamSynchronize(st));
@@ -374,19 +419,21 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     BinningState bin = binning_state_from(bin_base, (size_t)L);
     R3DG_CHECK_HIP(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, st));
     if (L > 0) {
-        hipLaunchKernelGGL(duplicate_keys_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, geom.means2D,
-                           geom.depths, geom.point_offsets, radii, gx, gy, bin.keys_unsorted, bin.gid_of_slot);
+        hipLaunchKernelGGL(duplicate_in_depth_order_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P,
+                           geom.depth_order, geom.depth_scan, geom.means2D, radii, gx, gy, bin.tile_keys,
+                           bin.gid_in);
         R3DG_CHECK_LAUNCH(s->debug, st);
+        // the reference sorts (tile << 32 | depth) over bits [0, 32 + msb(T)) (rasterizer_impl.cu:366-374);
+        // the depth part is already in order, so the tile bits [0, msb(T)) suffice
         const int bit = (int)higher_msb((uint32_t)T);
         size_t sb = bin.sort_temp_bytes;
         {
             ProfScope ps(R3DG_PROF_SORT, st);
-            R3DG_CHECK_HIP(rocprim::radix_sort_pairs(bin.sort_temp, sb, bin.keys_unsorted, bin.keys_sorted,
-                                                     rocprim::counting_iterator<uint32_t>(0), bin.sorted_slot,
-                                                     (size_t)L, 0, 32 + bit, st));
+            R3DG_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(bin.sort_temp, sb, bin.tile_keys, bin.tile_sorted,
+                                                                 bin.gid_in, bin.point_list, (size_t)L, 0, bit, st));
         }
-        hipLaunchKernelGGL(identify_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, st, L, bin.keys_sorted,
-                           bin.sorted_slot, bin.gid_of_slot, bin.point_list, img.ranges);
+        hipLaunchKernelGGL(identify_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, st, L, bin.tile_sorted,
+                           img.ranges);
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
@@ -441,7 +488,7 @@ extern "C" int r3dg_state_view(int P, int H, int W, int L, void* geom, void* bin
     GeomState gs = geom_state_from(geom, (size_t)P);
     BinningState bs = binning_state_from(binning, (size_t)L);
     ImageState is = image_state_from(image, H, W);
-    v->keys_sorted = bs.keys_sorted;
+    v->tile_sorted = bs.tile_sorted;
     v->point_list = bs.point_list;
     v->ranges = reinterpret_cast<const uint32_t*>(is.ranges);
     v->point_offsets = gs.point_offsets;
@@ -484,7 +531,8 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         RenderBwdArgs ba{};
         ba.ranges = is.ranges;
         ba.point_list = bs.point_list;
-        ba.sorted_slot = bs.sorted_slot;
+        ba.offsets = gs.point_offsets;
+        ba.radii = radii;
         ba.means2D = gs.means2D;
         ba.conic_opacity = gs.conic_opacity;
         ba.depths = gs.depths;
@@ -503,7 +551,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         ba.dL_dpix_d = gr->dL_dout_depth;
         ba.dL_dpix_f = gr->dL_dout_feature;
         ba.gflay = make_feature_layout(S, HW, gr->feature_native != 0);
-        ba.S = S; ba.W = W; ba.H = H; ba.grid_x = gx; ba.num_tiles = T; ba.cull = 1;
+        ba.S = S; ba.W = W; ba.H = H; ba.grid_x = gx; ba.grid_y = gy; ba.num_tiles = T; ba.cull = 1;
         if (const char* e = getenv("R3DG_NO_CULL")) ba.cull = (e[0] == '0');
         ba.backward_geometry = backward_geometry;
         ba.RS = RS;

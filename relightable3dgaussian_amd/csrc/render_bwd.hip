@@ -106,7 +106,9 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
     const int max_last = s_max_last;
     const int RS = a.RS;
     for (int p = max_last + t; p < n; p += kBlock) {
-        float4* row = reinterpret_cast<float4*>(a.rows + (size_t)a.sorted_slot[range.x + p] * RS);
+        const uint32_t gid = a.point_list[range.x + p];
+        const uint32_t slot = instance_slot(a.offsets, a.means2D[gid], a.radii[gid], gid, tx, ty, a.grid_x, a.grid_y);
+        float4* row = reinterpret_cast<float4*>(a.rows + (size_t)slot * RS);
         for (int q = 0; q < RS / 4; ++q) row[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
@@ -116,8 +118,8 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
         if (t < cnt) {
             const uint32_t k = range.x + (uint32_t)(hi - 1 - t);
             const uint32_t gid = a.point_list[k];
-            s_slot[t] = a.sorted_slot[k];
             const float2 xy = a.means2D[gid];
+            s_slot[t] = instance_slot(a.offsets, xy, a.radii[gid], gid, tx, ty, a.grid_x, a.grid_y);
             const float4 co = a.conic_opacity[gid];
             s_xy[t] = xy;
             s_co[t] = co;
@@ -362,7 +364,9 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
     const int max_last = s_max_last;
     const int RS = a.RS;
     for (int p = max_last + t; p < n; p += kBlock) {
-        float4* row = reinterpret_cast<float4*>(a.rows + (size_t)a.sorted_slot[range.x + p] * RS);
+        const uint32_t gid = a.point_list[range.x + p];
+        const uint32_t slot = instance_slot(a.offsets, a.means2D[gid], a.radii[gid], gid, tx, ty, a.grid_x, a.grid_y);
+        float4* row = reinterpret_cast<float4*>(a.rows + (size_t)slot * RS);
         for (int q = 0; q < RS / 4; ++q) row[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     // partial-row slot of each X channel / Y moment (col l&15 of the MFMA result)
@@ -385,8 +389,8 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
         if (t < cnt) {
             const uint32_t k = range.x + (uint32_t)(hi - 1 - t);
             const uint32_t gid = a.point_list[k];
-            s_slot[t] = a.sorted_slot[k];
             const float2 xy = a.means2D[gid];
+            s_slot[t] = instance_slot(a.offsets, xy, a.radii[gid], gid, tx, ty, a.grid_x, a.grid_y);
             const float4 co = a.conic_opacity[gid];
             s_xy[t] = xy;
             s_co[t] = co;

@@ -442,8 +442,16 @@ std::vector<torch::Tensor> rasterizer_state(const torch::Tensor& geomBuffer, con
         return buf.narrow(0, off, nbytes);
     };
     const int64_t T = ((W + 15) / 16) * ((H + 15) / 16);
-    return {slice(binningBuffer, v.keys_sorted, 8 * L).view(torch::kInt64),
-            slice(binningBuffer, v.point_list, 4 * L).view(torch::kInt32),
+    // the reference's sort key, rebuilt: tile << 32 | float bits of the instance's depth
+    auto plist = slice(binningBuffer, v.point_list, 4 * L).view(torch::kInt32);
+    auto dbits = slice(geomBuffer, v.depths, 4 * P).view(torch::kInt32).to(torch::kInt64).bitwise_and(0xffffffffLL);
+    auto keys = slice(binningBuffer, v.tile_sorted, 4 * L)
+                    .view(torch::kInt32)
+                    .to(torch::kInt64)
+                    .bitwise_left_shift(32)
+                    .bitwise_or(dbits.index_select(0, plist.to(torch::kInt64)));
+    return {keys,
+            plist,
             slice(imageBuffer, v.ranges, 8 * T).view(torch::kInt32).view({T, 2}),
             slice(geomBuffer, v.point_offsets, 4 * P).view(torch::kInt32),
             slice(geomBuffer, v.depths, 4 * P).view(torch::kFloat32),
