@@ -170,6 +170,8 @@ __device__ __forceinline__ float wave_sum_to_lane63(float v) {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+typedef float floatx4 __attribute__((ext_vector_type(4)));  // MFMA accumulator fragment
+
 // Exponent of the 2D Gaussian at offset (dx, dy) from its centre: -0.5 (a dx^2 + c dy^2) - b dx dy
 // (forward.cu:478, backward.cu:530). One fixed FMA pattern, so every call site -- forward and
 // backward, first or second instance of an unrolled pair -- rounds identically.

@@ -256,7 +256,6 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
 // instance. w and q go through a padded LDS image (row stride 66 floats: conflict-free for
 // both the row-wise writes and the column-wise A-operand reads).
 // ---------------------------------------------------------------------------------------------
-typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // Order this wave's LDS traffic for cross-lane exchange through LDS: wait for the wave's DS
 // operations and stop the compiler from moving memory accesses across (it cannot see lanes).
