@@ -181,4 +181,47 @@ __device__ __forceinline__ float gauss_power(float4 co, float dx, float dy) {
     return __builtin_fmaf(-0.5f, q, -((co.y * dx) * dy));
 }
 
+// Minimum of Q(d) = a dx^2 + 2b dx dy + c dy^2 (positive definite) over mean - pixel offsets with
+// the pixel in the rectangle [xa, xb] x [ya, yb]: 0 if the mean lies inside, else the smallest of
+// the four edge minima (each a clamped 1-D convex quadratic).
+__device__ __forceinline__ float qform_min_rect(float a, float b, float c, float ia, float ic, float mx, float my,
+                                                float xa, float xb, float ya, float yb) {
+    if (mx >= xa && mx <= xb && my >= ya && my <= yb) return 0.0f;
+    auto q = [&](float dx, float dy) { return a * dx * dx + 2.0f * b * dx * dy + c * dy * dy; };
+    auto edge_x = [&](float px) {  // pixel column fixed
+        const float dx = mx - px;
+        const float dy = fminf(fmaxf(-b * dx * ic, my - yb), my - ya);
+        return q(dx, dy);
+    };
+    auto edge_y = [&](float py) {  // pixel row fixed
+        const float dy = my - py;
+        const float dx = fminf(fmaxf(-b * dy * ia, mx - xb), mx - xa);
+        return q(dx, dy);
+    };
+    return fminf(fminf(edge_x(xa), edge_x(xb)), fminf(edge_y(ya), edge_y(yb)));
+}
+
+// Conservative set of the 8x8 quadrants of tile (x0, y0) in which alpha = o exp(-Q/2) can reach
+// 1/255, i.e. Q <= 2 ln(255 o). A quadrant is dropped only if the minimum of Q over its pixel
+// rectangle exceeds t = 2 ln(255 o) * 1.1 + 0.1 -- the 10 % + 0.1 margin covers the fp32
+// rounding of the blend's power and of __expf, so a dropped instance fails the reference's
+// alpha test on every pixel of the quadrant (tests/test_gpu_parity.py: cull on == off bitwise).
+__device__ __forceinline__ uint32_t quadrant_mask(float2 xy, float4 co, int x0, int y0, int cull) {
+    if (!cull) return 0xFu;
+    if (co.w < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 everywhere
+    const float det = co.x * co.z - co.y * co.y;
+    if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return 0xFu;
+    const float t = 2.0f * __logf(255.0f * co.w) * 1.1f + 0.1f;
+    if (!(t < 1e30f)) return 0xFu;
+    const float ia = 1.0f / co.x, ic = 1.0f / co.z;
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float qx = (float)(x0 + (q & 1) * 8), qy = (float)(y0 + (q >> 1) * 8);
+        const float qmin = qform_min_rect(co.x, co.y, co.z, ia, ic, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f);
+        if (!(qmin > t)) m |= 1u << q;
+    }
+    return m;
+}
+
 }  // namespace r3dg

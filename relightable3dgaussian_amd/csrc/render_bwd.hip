@@ -20,25 +20,6 @@
 
 namespace r3dg {
 
-__device__ __forceinline__ uint32_t quadrant_mask_b(float2 xy, float4 co, int x0, int y0, int cull) {
-    // identical test to render_fwd.hip quadrant_mask (see the derivation there)
-    if (!cull) return 0xFu;
-    if (co.w < 1.0f / 255.0f) return 0u;
-    const float det = co.x * co.z - co.y * co.y;
-    if (!(det > 0.0f)) return 0xFu;
-    const float t = 2.0f * __logf(255.0f * co.w) * 1.1f + 0.1f;
-    const float ex = sqrtf(t * co.z / det) + 1.0f;
-    const float ey = sqrtf(t * co.x / det) + 1.0f;
-    if (!(ex < 1e30f) || !(ey < 1e30f)) return 0xFu;
-    uint32_t m = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float qx = (float)(x0 + (q & 1) * 8), qy = (float)(y0 + (q >> 1) * 8);
-        if (xy.x + ex >= qx && xy.x - ex <= qx + 7.0f && xy.y + ey >= qy && xy.y - ey <= qy + 7.0f) m |= 1u << q;
-    }
-    return m;
-}
-
 __device__ __forceinline__ int wave_max_int(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
@@ -123,7 +104,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
             const float4 co = a.conic_opacity[gid];
             s_xy[t] = xy;
             s_co[t] = co;
-            s_mask[t] = quadrant_mask_b(xy, co, tx * kTileX, ty * kTileY, a.cull);
+            s_mask[t] = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
             float v[NA4 * 4];
 #pragma unroll
             for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
@@ -393,7 +374,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
             const float4 co = a.conic_opacity[gid];
             s_xy[t] = xy;
             s_co[t] = co;
-            m = quadrant_mask_b(xy, co, tx * kTileX, ty * kTileY, a.cull);
+            m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
             float v[NA4 * 4];
 #pragma unroll
             for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;

@@ -6,7 +6,8 @@
 //   * each batch of 256 sorted instances is staged in LDS once: xy, conic|opacity, and an AoS
 //     attribute row (colour, depth, [shader colour], features) read with ds_read_b128
 //     broadcasts -- the reference re-reads colours and features from HBM per pixel;
-//   * a conservative per-quadrant footprint mask (alpha >= 1/255 ellipse, widened) decides
+//   * a conservative per-quadrant footprint mask (minimum of the conic form over the quadrant
+//     against the widened alpha >= 1/255 threshold, r3dg_common.h quadrant_mask) decides
 //     which instances a wave visits. Skipping is exact: a skipped instance would have failed
 //     the reference's alpha test on every pixel of the quadrant (tests/test_gpu_parity.py
 //     checks cull on == cull off bit for bit). The masks are compacted at staging time into
@@ -18,29 +19,6 @@
 #include "r3dg_kernels.h"
 
 namespace r3dg {
-
-// Conservative set of 8x8 quadrants of tile (x0,y0) in which alpha = o*exp(power) can reach
-// 1/255. power = -Q/2 with Q = a dx^2 + 2b dx dy + c dy^2; alpha >= 1/255 needs
-// Q <= t = 2 ln(255 o). The ellipse Q <= t has half extents sqrt(t * cov_xx), sqrt(t * cov_yy)
-// with cov = conic^-1. Widened by 10 % + 0.1 in t and 1 px in extent to cover fp32 rounding
-// of power and __expf.
-__device__ __forceinline__ uint32_t quadrant_mask(float2 xy, float4 co, int x0, int y0, int cull) {
-    if (!cull) return 0xFu;
-    if (co.w < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 everywhere
-    const float det = co.x * co.z - co.y * co.y;
-    if (!(det > 0.0f)) return 0xFu;
-    const float t = 2.0f * __logf(255.0f * co.w) * 1.1f + 0.1f;
-    const float ex = sqrtf(t * co.z / det) + 1.0f;
-    const float ey = sqrtf(t * co.x / det) + 1.0f;
-    if (!(ex < 1e30f) || !(ey < 1e30f)) return 0xFu;
-    uint32_t m = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float qx = (float)(x0 + (q & 1) * 8), qy = (float)(y0 + (q >> 1) * 8);
-        if (xy.x + ex >= qx && xy.x - ex <= qx + 7.0f && xy.y + ey >= qy && xy.y - ey <= qy + 7.0f) m |= 1u << q;
-    }
-    return m;
-}
 
 template <int SMAX, bool SHADER>
 __global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
