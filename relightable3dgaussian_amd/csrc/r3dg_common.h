@@ -171,6 +171,7 @@ __device__ __forceinline__ float wave_sum_to_lane63(float v) {
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));  // MFMA accumulator fragment
+typedef float f32x2 __attribute__((ext_vector_type(2)));    // packed fp32 pair (v_pk_* ops)
 
 // Exponent of the 2D Gaussian at offset (dx, dy) from its centre: -0.5 (a dx^2 + c dy^2) - b dx dy
 // (forward.cu:478, backward.cu:530). One fixed FMA pattern, so every call site -- forward and
@@ -213,7 +214,8 @@ __device__ __forceinline__ uint32_t quadrant_mask(float2 xy, float4 co, int x0, 
     if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return 0xFu;
     const float t = 2.0f * __logf(255.0f * co.w) * 1.1f + 0.1f;
     if (!(t < 1e30f)) return 0xFu;
-    const float ia = 1.0f / co.x, ic = 1.0f / co.z;
+    // approximate reciprocals: an inexact minimiser changes Q only at second order
+    const float ia = __builtin_amdgcn_rcpf(co.x), ic = __builtin_amdgcn_rcpf(co.z);
     uint32_t m = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
