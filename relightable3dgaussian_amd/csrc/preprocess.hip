@@ -97,7 +97,24 @@ __device__ static float3 compute_cov2d(float3 mean, float fx, float fy, float ta
 
 // forward.cu:161-267 (preprocessCUDA)
 __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    // The block's SH coefficients (<= 48 floats per Gaussian) arrive by one coalesced copy into
+    // LDS (odd stride: conflict-free per-thread reads) instead of 48 strided loads per thread.
+    constexpr int SHS = 49;
+    __shared__ float s_sh[256 * SHS];
+    const int t = threadIdx.x;
+    const int g0 = blockIdx.x * 256;
+    const int idx = g0 + t;
+    const int M3 = 3 * a.M;
+    const bool use_sh = a.sh && !a.colors_precomp;
+    if (use_sh) {
+        const int ng = min(256, a.P - g0);
+        const float* src = a.sh + (size_t)g0 * M3;
+        for (int f = t; f < ng * M3; f += 256) {
+            const int gg = f / M3;
+            s_sh[gg * SHS + (f - gg * M3)] = src[f];
+        }
+    }
+    __syncthreads();
     if (idx >= a.P) return;
     a.radii[idx] = 0;
     a.tiles_touched[idx] = 0;
@@ -134,8 +151,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     int x0, y0, x1, y1;
     get_rect(px, py, (int)my_radius, a.grid_x, a.grid_y, x0, y0, x1, y1);
     if ((x1 - x0) * (y1 - y0) == 0) return;
-    if (!a.colors_precomp)
-        color_from_sh(a.D, p, a.campos, a.sh + (size_t)idx * a.M * 3, a.rgb + 3 * idx, a.clamped + idx);
+    if (use_sh) color_from_sh(a.D, p, a.campos, s_sh + t * SHS, a.rgb + 3 * idx, a.clamped + idx);
     a.depths[idx] = pv.z;
     a.radii[idx] = (int)my_radius;
     a.means2D[idx] = make_float2(px, py);
