@@ -75,6 +75,69 @@ def cpu_baseline(scene) -> dict:
                       f"preprocess+sort+blend fwd+bwd, {dt:.1f} s"}
 
 
+def brdf_c1(dev) -> dict:
+    """north_star's CPU leg: the reference's pure-PyTorch render equation (restated in
+    oracle/brdf_torch.py, pinned by tests/golden/brdf.npz) on SURVEY §8d config C1 (P = 10k,
+    Ns = 24, eval), fwd and fwd+bwd (loss = sum pbr + sum diffuse_light), median of 5 after 1
+    warmup, on this host's CPU share; next to this build's HIP kernels on the same inputs."""
+    import torch
+
+    from oracle import brdf_torch
+
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores) or cores))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    inp = brdf_torch.c1_inputs(10_000, seed=0)
+    keys = ["base", "rough", "metal", "normals", "viewdirs", "incidents", "env", "visibility"]
+
+    def cpu_fwd(grad):
+        t = {k: v.clone().requires_grad_(grad) for k, v in inp.items()}
+        pbr, ex = brdf_torch.rendering_equation(*[t[k] for k in keys], 24)
+        if grad:
+            (pbr.sum() + ex["diffuse_light"].sum()).backward()
+
+    def med(fn, n=5):
+        fn()
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e3
+
+    cpu_f, cpu_fb = med(lambda: cpu_fwd(False)), med(lambda: cpu_fwd(True))
+    torch.set_num_threads(prev)
+
+    import relightable3dgaussian_amd as r3
+
+    g = [inp[k].to(dev) for k in keys]
+    ones = torch.ones(10_000, 3, device=dev)
+
+    def gpu(grad):
+        pbr, dirs, dl = r3._C.render_equation_forward(*g, 24, False, False)
+        if grad:
+            r3._C.render_equation_backward(*g, 24, dirs, ones, ones, False)
+
+    def gmed(fn, n=20):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(n):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        return float(np.median(ts))
+
+    return {"config": "C1: P=10000, Ns=24, eval, synthetic inputs (SURVEY §8d)", "cores": cores, "kind": "port",
+            "cpu_fwd_ms": round(cpu_f, 3), "cpu_fwd_bwd_ms": round(cpu_fb, 3),
+            "gpu_fwd_ms": round(gmed(lambda: gpu(False)), 4), "gpu_fwd_bwd_ms": round(gmed(lambda: gpu(True)), 4),
+            "sample": "oracle/brdf_torch.py: PyTorch-CPU restatement of gaussian_renderer/neilf.py:437-519"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -198,6 +261,7 @@ def main() -> None:
     }
     if not args.no_cpu_baseline and world == 1:
         res["cpu_baseline"] = cpu_baseline(scene)
+        res["brdf_cpu_baseline"] = brdf_c1(dev)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
