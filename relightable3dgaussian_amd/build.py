@@ -60,7 +60,8 @@ def build_hip(jobs: int = 8) -> str:
         o = os.path.join(OBJ, src.replace(".hip", ".o"))
         objs.append(o)
         if _newer(o, [s] + hdrs + [__file__]):
-            cmds.append([HIPCC, "-c", s, "-o", o] + HIP_FLAGS + PER_FILE_FLAGS.get(src, []))
+            extra = os.environ.get("R3DG_EXTRA_HIPFLAGS", "").split()  # experiment builds only
+            cmds.append([HIPCC, "-c", s, "-o", o] + HIP_FLAGS + PER_FILE_FLAGS.get(src, []) + extra)
     with ThreadPoolExecutor(max(1, jobs)) as ex:
         list(ex.map(_run, cmds))
     so = os.path.join(LIB, "libr3dg_hip.so")

@@ -238,4 +238,10 @@ __global__ void __launch_bounds__(256) identify_ranges_kernel(int L, const uint3
     if (idx == L - 1) ranges[cur].y = L;
 }
 
+__global__ void __launch_bounds__(256) tile_count_kernel(int T, const uint2* __restrict__ ranges,
+                                                         uint32_t* __restrict__ counts) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < T) counts[t] = ranges[t].y - ranges[t].x;
+}
+
 }  // namespace r3dg

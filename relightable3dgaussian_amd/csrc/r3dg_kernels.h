@@ -42,6 +42,7 @@ struct RenderFwdArgs {
     const float* features;
     const float* bg;
     int S, W, H, grid_x, num_tiles, cull;
+    const uint32_t* tile_order;  // launch order of the tiles (longest first), or null
     float* final_T;
     uint32_t* n_contrib;
     float* out_color;
@@ -77,6 +78,7 @@ struct RenderBwdArgs {
     const float* dL_dpix_f;    // feature grads, layout gflay
     FeatureLayout gflay;
     int S, W, H, grid_x, grid_y, num_tiles, cull, backward_geometry, RS;
+    const uint32_t* tile_order;  // launch order of the tiles (longest first), or null
     float* rows;               // [L, RS]
 };
 
@@ -163,5 +165,14 @@ __device__ __forceinline__ int xcd_tile(int b, int grid) {
     const int per = grid >> 3;
     return (b & 7) * per + (b >> 3);
 }
+// Tile of workgroup b: longest tiles first when an order is given (workgroups are dispatched in
+// index order, so the heaviest tiles start first and the tail is made of short tiles), else the
+// XCD-aware spatial order.
+__device__ __forceinline__ int block_tile(const uint32_t* order, int num_tiles) {
+    const int b = blockIdx.x;
+    if (order) return b < num_tiles ? (int)order[b] : num_tiles;
+    return xcd_tile(b, gridDim.x);
+}
+__global__ void tile_count_kernel(int T, const uint2* ranges, uint32_t* counts);
 
 }  // namespace r3dg

@@ -75,6 +75,18 @@ static size_t depth_sort_temp_size(size_t P) {  // depth sort of the Gaussians
     return bytes;
 }
 
+static size_t tile_order_temp_size(size_t T) {
+    size_t bytes = 0;
+    uint32_t* k = nullptr;
+    rocprim::radix_sort_pairs_desc(nullptr, bytes, k, k, rocprim::counting_iterator<uint32_t>(0), k, T, 0, 32, 0);
+    return bytes;
+}
+
+static bool use_tile_order() {
+    const char* e = getenv("R3DG_TILE_ORDER");
+    return !(e && e[0] == 'x');  // backward: "xcd" = spatial XCD-aware order; default longest first
+}
+
 static auto depth_order_touched(const uint32_t* touched, const uint32_t* order) {
     return rocprim::make_transform_iterator(rocprim::counting_iterator<uint32_t>(0),
                                             TouchedInDepthOrder{touched, order});
@@ -154,7 +166,13 @@ static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end) {
     const size_t N = (size_t)H * W;
     s.final_T = carve<float>(p, N);
     s.n_contrib = carve<uint32_t>(p, N);
-    s.ranges = carve<uint2>(p, (size_t)num_tiles_of(H, W));
+    const size_t T = (size_t)num_tiles_of(H, W);
+    s.ranges = carve<uint2>(p, T);
+    s.tile_count = carve<uint32_t>(p, T);
+    s.tile_count_sorted = carve<uint32_t>(p, T);
+    s.tile_order = carve<uint32_t>(p, T);
+    s.order_temp_bytes = tile_order_temp_size(T);
+    s.order_temp = carve<char>(p, s.order_temp_bytes);
     if (end) *end = p;
     return s;
 }
@@ -436,6 +454,15 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
                            img.ranges);
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
+    const bool order_tiles = use_tile_order();
+    {  // always computed (cheap), so a backward may use it whatever the forward's setting
+        hipLaunchKernelGGL(tile_count_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, img.ranges, img.tile_count);
+        size_t ob = img.order_temp_bytes;
+        R3DG_CHECK_HIP(rocprim::radix_sort_pairs_desc(img.order_temp, ob, img.tile_count, img.tile_count_sorted,
+                                                      rocprim::counting_iterator<uint32_t>(0), img.tile_order,
+                                                      (size_t)T, 0, 32, st));
+        R3DG_CHECK_LAUNCH(s->debug, st);
+    }
 
     // stencil: default shaders give all-zero stencil values (InitializeStencil, rasterizer_impl.cu:203-209)
     if (out->stencil) R3DG_CHECK_HIP(hipMemsetAsync(out->stencil, 0, sizeof(float) * (size_t)H * W, st));
@@ -451,6 +478,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     ra.features = g->features;
     ra.bg = s->bg;
     ra.S = S; ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = T; ra.cull = 1;
+    ra.tile_order = nullptr;  // forward: XCD-aware spatial order (measured faster: L2 locality)
+    (void)order_tiles;
     ra.final_T = img.final_T;
     ra.n_contrib = img.n_contrib;
     ra.out_color = out->color;
@@ -552,6 +581,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         ba.dL_dpix_f = gr->dL_dout_feature;
         ba.gflay = make_feature_layout(S, HW, gr->feature_native != 0);
         ba.S = S; ba.W = W; ba.H = H; ba.grid_x = gx; ba.grid_y = gy; ba.num_tiles = T; ba.cull = 1;
+        ba.tile_order = use_tile_order() ? is.tile_order : nullptr;
         if (const char* e = getenv("R3DG_NO_CULL")) ba.cull = (e[0] == '0');
         ba.backward_geometry = backward_geometry;
         ba.RS = RS;

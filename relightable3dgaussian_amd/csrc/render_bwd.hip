@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
     __shared__ int s_max_last;
     float* s_part = reinterpret_cast<float*>(s_part4);
 
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int tile = block_tile(a.tile_order, a.num_tiles);
     if (tile >= a.num_tiles) return;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
     __shared__ int s_max_last;
     float* s_part = reinterpret_cast<float*>(s_part4);
 
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int tile = block_tile(a.tile_order, a.num_tiles);
     if (tile >= a.num_tiles) return;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;

@@ -29,7 +29,7 @@ __global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
     __shared__ float4 s_attr[kBlock * NA4];
     __shared__ uint32_t s_bits[8][4];                  // [32-instance chunk][wave]: live-instance masks
 
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int tile = block_tile(a.tile_order, a.num_tiles);
     if (tile >= a.num_tiles) return;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
