@@ -158,6 +158,22 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     a.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, a.opacity[idx]);
     a.tiles_touched[idx] = (uint32_t)((y1 - y0) * (x1 - x0));
     a.depth_keys[idx] = __float_as_uint(pv.z);
+    if (a.records) {  // render record (r3dg_kernels.h record_f4); slot0 follows in the duplicate pass
+        float4* rec = a.records + (size_t)idx * a.rec4;
+        rec[0] = make_float4(conic.x, conic.y, conic.z, a.opacity[idx]);
+        rec[1] = make_float4(px, py, 0.0f, __int_as_float((int)my_radius));
+        const float* col = a.colors_precomp ? a.colors_precomp + 3 * idx : a.rgb + 3 * idx;
+        const float* f = a.features ? a.features + (size_t)idx * a.S : nullptr;
+        for (int q = 0; q < a.rec4 - 2; ++q) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = 4 * q + e;
+                v[e] = c < 3 ? col[c] : (c == 3 ? pv.z : (c - 4 < a.S ? f[c - 4] : 0.0f));
+            }
+            rec[2 + q] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
 }
 
 // rasterizer_impl.cu:56-68 (checkFrustum)
@@ -181,7 +197,8 @@ __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* _
 __global__ void __launch_bounds__(256) duplicate_in_depth_order_kernel(
     int P, const uint32_t* __restrict__ order, const uint32_t* __restrict__ depth_scan,
     const float2* __restrict__ means2D, const int* __restrict__ radii, int grid_x, int grid_y,
-    uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ gid_out) {
+    uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ gid_out, const uint32_t* __restrict__ offsets,
+    float4* __restrict__ records, int rec4) {
     __shared__ uint32_t s_end[256];  // inclusive end of each Gaussian's instances, block-relative
     __shared__ uint32_t s_gid[256];
     __shared__ int s_x0[256], s_y0[256], s_w[256];
@@ -198,6 +215,9 @@ __global__ void __launch_bounds__(256) duplicate_in_depth_order_kernel(
         if (r > 0) {
             const float2 m = means2D[g];
             get_rect(m.x, m.y, r, grid_x, grid_y, x0, y0, x1, y1);
+            if (records)  // the Gaussian's first unsorted slot, for the backward's rows
+                reinterpret_cast<float*>(records + (size_t)g * rec4 + 1)[2] =
+                    __uint_as_float(g == 0 ? 0u : offsets[g - 1]);
         }
         s_x0[t] = x0;
         s_y0[t] = y0;

@@ -66,6 +66,9 @@ struct GeomState {
     size_t depth_sort_temp_bytes;
     void* depth_scan_temp;
     size_t depth_scan_temp_bytes;
+    // [P, record_f4(S)] render records, last in the buffer (r3dg_kernels.h): only set when the
+    // state is carved with S
+    float4* records;
 };
 
 // tiles_touched of the i-th Gaussian in depth order (input of the depth-order scan)
@@ -96,10 +99,10 @@ struct ImageState {
     size_t order_temp_bytes;
 };
 
-size_t geom_state_bytes(size_t P);
+size_t geom_state_bytes(size_t P, int S);
 size_t binning_state_bytes(size_t L);
 size_t image_state_bytes(int H, int W);
-GeomState geom_state_from(void* base, size_t P);
+GeomState geom_state_from(void* base, size_t P, int S = -1);
 BinningState binning_state_from(void* base, size_t L);
 ImageState image_state_from(void* base, int H, int W);
 

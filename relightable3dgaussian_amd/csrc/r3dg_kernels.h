@@ -22,6 +22,9 @@ struct PreprocessArgs {
     int* radii;
     uint32_t* tiles_touched;
     uint32_t* depth_keys;  // float bits of the view depth, 0xffffffff when not visible
+    float4* records;       // [P, rec4] render records (see record_f4)
+    int rec4, S;
+    const float* features; // [P, S]
     float* depths;
     float2* means2D;
     float* cov3D;
@@ -32,6 +35,7 @@ struct PreprocessArgs {
 };
 
 struct RenderFwdArgs {
+    const float4* records;     // render records (record_f4), used by the default-shader kernel
     const uint2* ranges;
     const uint32_t* point_list;
     const float2* means2D;
@@ -59,6 +63,7 @@ constexpr int kRowMean = 0, kRowConic = 3, kRowOpacity = 6, kRowColor = 7, kRowF
 __host__ __device__ inline int row_stride(int S) { return ((kRowFeat + S) + 3) & ~3; }
 
 struct RenderBwdArgs {
+    const float4* records;     // render records (record_f4)
     const uint2* ranges;
     const uint32_t* point_list;
     const uint32_t* offsets;   // inclusive scan of tiles touched: Gaussian g owns slots [offsets[g-1], offsets[g])
@@ -138,8 +143,16 @@ __global__ void preprocess_kernel(PreprocessArgs a);
 __global__ void mark_visible_kernel(int P, const float* means3D, const float* view, uint8_t* present);
 __global__ void duplicate_in_depth_order_kernel(int P, const uint32_t* order, const uint32_t* depth_scan,
                                                 const float2* means2D, const int* radii, int grid_x, int grid_y,
-                                                uint32_t* tile_keys, uint32_t* gid_out);
+                                                uint32_t* tile_keys, uint32_t* gid_out, const uint32_t* offsets,
+                                                float4* records, int rec4);
 __global__ void identify_ranges_kernel(int L, const uint32_t* tiles, uint2* ranges);
+
+// Slot of an instance from its Gaussian's render record word 1 (x, y, slot0, radius) and its tile.
+__device__ __forceinline__ uint32_t record_slot(float4 r1, int tx, int ty, int grid_x, int grid_y) {
+    int x0, y0, x1, y1;
+    get_rect(r1.x, r1.y, __float_as_int(r1.w), grid_x, grid_y, x0, y0, x1, y1);
+    return __float_as_uint(r1.z) + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
+}
 
 // Slot of the instance (Gaussian g, tile) in the reference's unsorted, Gaussian-contiguous order:
 // offsets[g-1] + row-major index of the tile in g's rect (duplicateWithKeys, rasterizer_impl.cu:92-107).
@@ -160,6 +173,17 @@ hipError_t launch_gather_backward(const GatherBwdArgs& a, hipStream_t stream);
 // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so block b runs on the
 // same XCD as b+8. Give each XCD a contiguous band of tiles (neighbouring tiles share
 // Gaussians, so their attribute gathers hit the same L2). Grid is padded to a multiple of 8.
+// Feature-count bucket of the templated blend kernels (launch_* dispatch) and the per-Gaussian
+// render record the blend kernels stage from: float4 [conic.x, conic.y, conic.z, opacity],
+// float4 [x, y, slot0 bits, radius bits], then the attribute row [r, g, b, depth, f0 .. f_{SMAX-1}]
+// zero-padded to (4 + SMAX + 3) / 4 float4. slot0 = offsets[g-1] (the Gaussian's first unsorted
+// slot). Written by preprocess_kernel (+ slot0 by duplicate_in_depth_order_kernel) for visible
+// Gaussians only; the blend kernels never stage an invisible one.
+__host__ __device__ inline int smax_of(int S) {
+    return S == 0 ? 0 : S <= 4 ? 4 : S <= 8 ? 8 : S <= 12 ? 12 : S <= 16 ? 16 : S <= 24 ? 24 : 32;
+}
+__host__ __device__ inline int record_f4(int S) { return 2 + (4 + smax_of(S) + 3) / 4; }
+
 __host__ __device__ inline int padded_tile_grid(int num_tiles) { return (num_tiles + 7) & ~7; }
 __device__ __forceinline__ int xcd_tile(int b, int grid) {
     const int per = grid >> 3;

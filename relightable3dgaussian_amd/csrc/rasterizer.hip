@@ -107,7 +107,7 @@ static T* carve(uintptr_t& p, size_t count) {
     return r;
 }
 
-static GeomState carve_geom(uintptr_t p, size_t P, uintptr_t* end) {
+static GeomState carve_geom(uintptr_t p, size_t P, int S, uintptr_t* end) {
     GeomState g{};
     g.depths = carve<float>(p, P);
     g.internal_radii = carve<int>(p, P);
@@ -131,15 +131,17 @@ static GeomState carve_geom(uintptr_t p, size_t P, uintptr_t* end) {
     g.depth_sort_temp = carve<char>(p, g.depth_sort_temp_bytes);
     g.depth_scan_temp_bytes = depth_scan_temp_size(P);
     g.depth_scan_temp = carve<char>(p, g.depth_scan_temp_bytes);
+    // render records last: every other offset is independent of S
+    g.records = S >= 0 ? carve<float4>(p, P * (size_t)record_f4(S)) : nullptr;
     if (end) *end = p;
     return g;
 }
-size_t geom_state_bytes(size_t P) {
+size_t geom_state_bytes(size_t P, int S) {
     uintptr_t end = 0;
-    carve_geom(0, P, &end);
+    carve_geom(0, P, S, &end);
     return (size_t)end;
 }
-GeomState geom_state_from(void* base, size_t P) { return carve_geom((uintptr_t)base, P, nullptr); }
+GeomState geom_state_from(void* base, size_t P, int S) { return carve_geom((uintptr_t)base, P, S, nullptr); }
 
 static BinningState carve_binning(uintptr_t p, size_t L, uintptr_t* end) {
     BinningState b{};
@@ -374,13 +376,13 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
 
     const int gx = (W + kTileX - 1) / kTileX, gy = (H + kTileY - 1) / kTileY;
     const int T = gx * gy;
-    void* geom_base = geom_alloc(geom_ctx, geom_state_bytes((size_t)P));
+    void* geom_base = geom_alloc(geom_ctx, geom_state_bytes((size_t)P, S));
     void* img_base = image_alloc(image_ctx, image_state_bytes(H, W));
     if (!geom_base || !img_base) {
         set_error("rasterize_gaussians: state allocation failed");
         return R3DG_ERR_ALLOC;
     }
-    GeomState geom = geom_state_from(geom_base, (size_t)P);
+    GeomState geom = geom_state_from(geom_base, (size_t)P, S);
     ImageState img = image_state_from(img_base, H, W);
     int* radii = out->radii ? out->radii : geom.internal_radii;
     const float focal_y = H / (2.0f * s->tan_fovy);
@@ -397,6 +399,7 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         pa.sh = g->sh; pa.cov3D_precomp = g->cov3D_precomp; pa.colors_precomp = g->colors_precomp;
         pa.view = s->viewmatrix; pa.proj = s->projmatrix; pa.campos = s->campos;
         pa.radii = radii; pa.tiles_touched = geom.tiles_touched; pa.depth_keys = geom.depth_keys;
+        pa.records = geom.records; pa.rec4 = record_f4(S); pa.S = S; pa.features = g->features;
         pa.depths = geom.depths;
         pa.means2D = geom.means2D; pa.cov3D = geom.cov3D; pa.conic_opacity = geom.conic_opacity;
         pa.rgb = geom.rgb; pa.clamped = geom.clamped; pa.error_flag = nullptr;
@@ -439,7 +442,7 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     if (L > 0) {
         hipLaunchKernelGGL(duplicate_in_depth_order_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P,
                            geom.depth_order, geom.depth_scan, geom.means2D, radii, gx, gy, bin.tile_keys,
-                           bin.gid_in);
+                           bin.gid_in, geom.point_offsets, geom.records, record_f4(S));
         R3DG_CHECK_LAUNCH(s->debug, st);
         // the reference sorts (tile << 32 | depth) over bits [0, 32 + msb(T)) (rasterizer_impl.cu:366-374);
         // the depth part is already in order, so the tile bits [0, msb(T)) suffice
@@ -468,6 +471,7 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     if (out->stencil) R3DG_CHECK_HIP(hipMemsetAsync(out->stencil, 0, sizeof(float) * (size_t)H * W, st));
 
     RenderFwdArgs ra{};
+    ra.records = geom.records;
     ra.ranges = img.ranges;
     ra.point_list = bin.point_list;
     ra.means2D = geom.means2D;
@@ -545,7 +549,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     if (P == 0) return R3DG_OK;
     const int gx = (W + kTileX - 1) / kTileX, gy = (H + kTileY - 1) / kTileY;
     const int T = gx * gy;
-    GeomState gs = geom_state_from(geom, (size_t)P);
+    GeomState gs = geom_state_from(geom, (size_t)P, S);
     BinningState bs = binning_state_from(binning, (size_t)L);
     ImageState is = image_state_from(image, H, W);
     const int* radii = radii_in ? radii_in : gs.internal_radii;
@@ -558,6 +562,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
             return R3DG_ERR_ALLOC;
         }
         RenderBwdArgs ba{};
+        ba.records = gs.records;
         ba.ranges = is.ranges;
         ba.point_list = bs.point_list;
         ba.offsets = gs.point_offsets;

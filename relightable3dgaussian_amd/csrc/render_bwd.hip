@@ -246,7 +246,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 template <int SMAX>
-__global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? 3 : 1)))
+render_bwd_mfma_kernel(RenderBwdArgs a) {
     constexpr int NA4 = (4 + SMAX + 3) / 4;       // staged attribute row: colour, depth, features
     constexpr int NR = kRowFeat + SMAX;
     constexpr int RSL = (NR + 3) & ~3;            // LDS partial row stride (floats)
@@ -345,7 +346,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
     const int RS = a.RS;
     for (int p = max_last + t; p < n; p += kBlock) {
         const uint32_t gid = a.point_list[range.x + p];
-        const uint32_t slot = instance_slot(a.offsets, a.means2D[gid], a.radii[gid], gid, tx, ty, a.grid_x, a.grid_y);
+        const uint32_t slot = record_slot(a.records[(size_t)gid * (2 + NA4) + 1], tx, ty, a.grid_x, a.grid_y);
         float4* row = reinterpret_cast<float4*>(a.rows + (size_t)slot * RS);
         for (int q = 0; q < RS / 4; ++q) row[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -369,26 +370,16 @@ __global__ void __launch_bounds__(kBlock) render_bwd_mfma_kernel(RenderBwdArgs a
         if (t < cnt) {
             const uint32_t k = range.x + (uint32_t)(hi - 1 - t);
             const uint32_t gid = a.point_list[k];
-            const float2 xy = a.means2D[gid];
-            s_slot[t] = instance_slot(a.offsets, xy, a.radii[gid], gid, tx, ty, a.grid_x, a.grid_y);
-            const float4 co = a.conic_opacity[gid];
+            // one contiguous render record per Gaussian (r3dg_kernels.h record_f4)
+            const float4* rec = a.records + (size_t)gid * (2 + NA4);
+            const float4 co = rec[0], r1 = rec[1];
+            const float2 xy = make_float2(r1.x, r1.y);
+            s_slot[t] = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
             s_xy[t] = xy;
             s_co[t] = co;
             m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
-            float v[NA4 * 4];
 #pragma unroll
-            for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
-            v[0] = a.colors[3 * gid + 0];
-            v[1] = a.colors[3 * gid + 1];
-            v[2] = a.colors[3 * gid + 2];
-            v[3] = a.depths[gid];
-            const float* f = a.features + (size_t)gid * S;
-#pragma unroll
-            for (int c = 0; c < SMAX; ++c)
-                if (c < S) v[4 + c] = f[c];
-#pragma unroll
-            for (int q = 0; q < NA4; ++q)
-                s_attr[t * NA4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+            for (int q = 0; q < NA4; ++q) s_attr[t * NA4 + q] = rec[2 + q];
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {

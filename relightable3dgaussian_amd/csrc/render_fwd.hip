@@ -21,7 +21,8 @@
 namespace r3dg {
 
 template <int SMAX, bool SHADER>
-__global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? 6 : 1)))
+render_fwd_kernel(RenderFwdArgs a) {
     constexpr int FO = SHADER ? 8 : 4;                 // feature offset inside the attribute row
     constexpr int NA4 = (FO + SMAX + 3) / 4;           // float4 per attribute row
     __shared__ float2 s_xy[kBlock];
@@ -53,30 +54,42 @@ __global__ void __launch_bounds__(kBlock) render_fwd_kernel(RenderFwdArgs a) {
         uint32_t m = 0;
         if (base + t < n) {
             const uint32_t gid = a.point_list[range.x + base + t];
-            const float2 xy = a.means2D[gid];
-            const float4 co = a.conic_opacity[gid];
-            s_xy[t] = xy;
-            s_co[t] = co;
-            m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
-            float v[NA4 * 4];
+            if constexpr (!SHADER) {
+                // one contiguous render record per Gaussian (r3dg_kernels.h record_f4)
+                const float4* rec = a.records + (size_t)gid * (2 + NA4);
+                const float4 co = rec[0], r1 = rec[1];
+                const float2 xy = make_float2(r1.x, r1.y);
+                s_xy[t] = xy;
+                s_co[t] = co;
+                m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
 #pragma unroll
-            for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
-            v[0] = a.colors[3 * gid + 0];
-            v[1] = a.colors[3 * gid + 1];
-            v[2] = a.colors[3 * gid + 2];
-            v[3] = a.depths[gid];
-            if constexpr (SHADER) {
-                v[4] = a.shader_colors[3 * gid + 0];
-                v[5] = a.shader_colors[3 * gid + 1];
-                v[6] = a.shader_colors[3 * gid + 2];
+                for (int q = 0; q < NA4; ++q) s_attr[t * NA4 + q] = rec[2 + q];
+            } else {
+                const float2 xy = a.means2D[gid];
+                const float4 co = a.conic_opacity[gid];
+                s_xy[t] = xy;
+                s_co[t] = co;
+                m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
+                float v[NA4 * 4];
+#pragma unroll
+                for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
+                v[0] = a.colors[3 * gid + 0];
+                v[1] = a.colors[3 * gid + 1];
+                v[2] = a.colors[3 * gid + 2];
+                v[3] = a.depths[gid];
+                if constexpr (SHADER) {
+                    v[4] = a.shader_colors[3 * gid + 0];
+                    v[5] = a.shader_colors[3 * gid + 1];
+                    v[6] = a.shader_colors[3 * gid + 2];
+                }
+                const float* f = a.features + (size_t)gid * a.S;
+#pragma unroll
+                for (int c = 0; c < SMAX; ++c)
+                    if (c < a.S) v[FO + c] = f[c];
+#pragma unroll
+                for (int q = 0; q < NA4; ++q)
+                    s_attr[t * NA4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
             }
-            const float* f = a.features + (size_t)gid * a.S;
-#pragma unroll
-            for (int c = 0; c < SMAX; ++c)
-                if (c < a.S) v[FO + c] = f[c];
-#pragma unroll
-            for (int q = 0; q < NA4; ++q)
-                s_attr[t * NA4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
         }
         // compaction: this wave's 64 staged slots are chunks 2w and 2w+1; one ballot per target wave
 #pragma unroll
