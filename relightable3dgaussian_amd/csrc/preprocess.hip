@@ -95,27 +95,10 @@ __device__ static float3 compute_cov2d(float3 mean, float fx, float fy, float ta
                        g1[0] * v0 + g1[1] * v1 + g1[2] * v2 + 0.3f);
 }
 
-// forward.cu:161-267 (preprocessCUDA)
-__global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
-    // The block's SH coefficients (<= 48 floats per Gaussian) arrive by one coalesced copy into
-    // LDS (odd stride: conflict-free per-thread reads) instead of 48 strided loads per thread.
-    constexpr int SHS = 49;
-    __shared__ float s_sh[256 * SHS];
-    const int t = threadIdx.x;
-    const int g0 = blockIdx.x * 256;
-    const int idx = g0 + t;
-    const int M3 = 3 * a.M;
-    const bool use_sh = a.sh && !a.colors_precomp;
-    if (use_sh) {
-        const int ng = min(256, a.P - g0);
-        const float* src = a.sh + (size_t)g0 * M3;
-        for (int f = t; f < ng * M3; f += 256) {
-            const int gg = f / M3;
-            s_sh[gg * SHS + (f - gg * M3)] = src[f];
-        }
-    }
-    __syncthreads();
-    if (idx >= a.P) return;
+// forward.cu:161-267 (preprocessCUDA) for one Gaussian. Returns whether it is visible; when it is,
+// rec0/rec1/col/depth are the head of its render record (r3dg_kernels.h record_f4).
+__device__ static bool preprocess_one(const PreprocessArgs& a, int idx, const float* sh, float4& rec0, float4& rec1,
+                                      const float*& col, float& depth) {
     a.radii[idx] = 0;
     a.tiles_touched[idx] = 0;
     a.depth_keys[idx] = 0xffffffffu;
@@ -123,7 +106,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     const float3 pv = xform_point4x3(p, a.view);
     if (pv.z <= 0.2f) {  // auxiliary.h:154 (the reference __trap()s when prefiltered; we flag it)
         if (a.prefiltered && a.error_flag) atomicOr(a.error_flag, 1u);
-        return;
+        return false;
     }
     const float4 ph = xform_point4x4(p, a.proj);
     const float p_w = 1.0f / (ph.w + 0.0000001f);
@@ -140,7 +123,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     }
     const float3 cov = compute_cov2d(p, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, cov3D, a.view);
     const float det = cov.x * cov.z - cov.y * cov.y;
-    if (det == 0.0f) return;
+    if (det == 0.0f) return false;
     const float det_inv = 1.f / det;
     const float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
     const float mid = 0.5f * (cov.x + cov.z);
@@ -150,33 +133,72 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     const float px = ndc2pix(ppx, a.W), py = ndc2pix(ppy, a.H);
     int x0, y0, x1, y1;
     get_rect(px, py, (int)my_radius, a.grid_x, a.grid_y, x0, y0, x1, y1);
-    if ((x1 - x0) * (y1 - y0) == 0) return;
-    if (use_sh) color_from_sh(a.D, p, a.campos, s_sh + t * SHS, a.rgb + 3 * idx, a.clamped + idx);
+    if ((x1 - x0) * (y1 - y0) == 0) return false;
+    if (!a.colors_precomp) color_from_sh(a.D, p, a.campos, sh, a.rgb + 3 * idx, a.clamped + idx);
     a.depths[idx] = pv.z;
     a.radii[idx] = (int)my_radius;
     a.means2D[idx] = make_float2(px, py);
-    a.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, a.opacity[idx]);
+    rec0 = make_float4(conic.x, conic.y, conic.z, a.opacity[idx]);
+    a.conic_opacity[idx] = rec0;
     a.tiles_touched[idx] = (uint32_t)((y1 - y0) * (x1 - x0));
     a.depth_keys[idx] = __float_as_uint(pv.z);
-    if (a.records) {  // render record (r3dg_kernels.h record_f4); slot0 follows in the duplicate pass
-        float4* rec = a.records + (size_t)idx * a.rec4;
-        rec[0] = make_float4(conic.x, conic.y, conic.z, a.opacity[idx]);
-        rec[1] = make_float4(px, py, 0.0f, __int_as_float((int)my_radius));
-        const float* col = a.colors_precomp ? a.colors_precomp + 3 * idx : a.rgb + 3 * idx;
-        const float* f = a.features ? a.features + (size_t)idx * a.S : nullptr;
-        for (int q = 0; q < a.rec4 - 2; ++q) {
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int c = 4 * q + e;
-                v[e] = c < 3 ? col[c] : (c == 3 ? pv.z : (c - 4 < a.S ? f[c - 4] : 0.0f));
-            }
-            rec[2 + q] = make_float4(v[0], v[1], v[2], v[3]);
-        }
-    }
+    rec1 = make_float4(px, py, 0.0f, __int_as_float((int)my_radius));  // slot0 set by the duplicate pass
+    col = a.colors_precomp ? a.colors_precomp + 3 * idx : a.rgb + 3 * idx;
+    depth = pv.z;
+    return true;
 }
 
-// rasterizer_impl.cu:56-68 (checkFrustum)
+__global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
+    // LDS: first the block's SH coefficients (one coalesced copy, odd stride: conflict-free
+    // per-thread reads), then the block's render records, assembled here and written out as one
+    // contiguous, coalesced span.
+    constexpr int SHS = 49;
+    __shared__ float4 s_buf4[256 * SHS / 4 + 1];
+    float* s_buf = reinterpret_cast<float*>(s_buf4);
+    const int t = threadIdx.x;
+    const int g0 = blockIdx.x * 256;
+    const int idx = g0 + t;
+    const int ng = min(256, a.P - g0);
+    const int M3 = 3 * a.M;
+    const bool use_sh = a.sh && !a.colors_precomp;
+    if (use_sh) {
+        const float* src = a.sh + (size_t)g0 * M3;
+        for (int f = t; f < ng * M3; f += 256) {
+            const int gg = f / M3;
+            s_buf[gg * SHS + (f - gg * M3)] = src[f];
+        }
+    }
+    __syncthreads();
+    float4 rec0, rec1;
+    const float* col = nullptr;
+    float depth = 0.f;
+    const bool vis = idx < a.P && preprocess_one(a, idx, s_buf + t * SHS, rec0, rec1, col, depth);
+    if (!a.records) return;
+    __syncthreads();  // SH consumed: the buffer now holds the records
+    const int RF = 4 * a.rec4;  // floats per record
+    if (vis) {
+        float* r = s_buf + t * RF;
+        reinterpret_cast<float4*>(r)[0] = rec0;
+        reinterpret_cast<float4*>(r)[1] = rec1;
+        reinterpret_cast<float4*>(r)[2] = make_float4(col[0], col[1], col[2], depth);
+    }
+    const int S = a.S, padf = RF - 12 - S;  // features at record float 12, then zero padding
+    if (S > 0) {
+        const float* src = a.features + (size_t)g0 * S;
+        for (int f = t; f < ng * S; f += 256) {
+            const int gg = f / S;
+            s_buf[gg * RF + 12 + (f - gg * S)] = src[f];
+        }
+    }
+    for (int f = t; f < ng * padf; f += 256) {
+        const int gg = f / padf;
+        s_buf[gg * RF + 12 + S + (f - gg * padf)] = 0.0f;
+    }
+    __syncthreads();
+    float4* dst = a.records + (size_t)g0 * a.rec4;
+    for (int f = t; f < ng * a.rec4; f += 256) dst[f] = s_buf4[f];
+}
+
 __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* __restrict__ means3D,
                                                            const float* __restrict__ view, uint8_t* present) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
