@@ -245,6 +245,20 @@ int r3dg_profile_enable(int max_records);
 int r3dg_profile_read(int kernel, int* count, float* total_ms);
 
 /* Texture mode helpers (utils/texture.cu EncodeTextureMode / EncodeWrapMode). */
+/* ---- textures (utils/texture.cu, asset_processing/textureImport.py) ----------------------- */
+/* AllocateTexture (texture.cu:86-101,103-226): a texture from a device pixel array [H, W, C],
+ * C the channel count of the PIL mode `mode` (r3dg_encode_texture_mode: 1 for 1/L/P/I/F, 3 for
+ * RGB/YCbCr/LAB/HSV, 4 for RGBA/CMYK). Stored as float4 texels (3-channel modes get alpha 1 as
+ * CreatPaddedArrayFromBase does) and sampled in software with the CUDA texture rules: wrap_u/v
+ * from r3dg_encode_wrap_mode, normalized or texel coordinates, bilinear filtering with 8-bit
+ * fractional weights (point sampling for LAB/HSV). Returns an opaque handle. */
+int r3dg_texture_create(const float* pixels, int width, int height, int mode, int wrap_u, int wrap_v,
+                        int normalized, int64_t* texture, r3dg_stream_t stream);
+/* UploadTexturesToDevice (texture.cu:237-246): named textures + the error texture a shader gets
+ * for a missing name (TextureManager::GetTexture, texture.cu:298-314). Shaders resolve their
+ * texture names against it at launch. */
+int r3dg_texture_manager_create(int n, const char* const* names, const int64_t* textures, int64_t error_texture,
+                                int64_t* manager);
 int r3dg_encode_texture_mode(const char* mode);
 int r3dg_encode_wrap_mode(const char* mode);
 

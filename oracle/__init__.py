@@ -24,8 +24,8 @@ F = np.float32
 
 
 def build() -> str:
-    src = os.path.join(HERE, "r3dg_oracle.c")
-    if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("r3dg_oracle.c", "r3dg_shaders.c", "Makefile")]
+    if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return _LIB
 
@@ -63,13 +63,94 @@ def planar_layout(S: int, HW: int):
 
 
 # ---------------------------------------------------------------------------------------------
+# textures and shaders (r3dg_shaders.c)
+# ---------------------------------------------------------------------------------------------
+# registry ids: the alphabetical name order of the shader maps (ShShader.cu:196-230,
+# splatShader.cu:283-333), the same ids the HIP registry hands out
+SH_CULLHALF, SH_EXPPOS, SH_GAUSSDISSOLVE, SH_HEARTBEAT, SH_DEFAULT = range(5)
+SH_NAMES = ["CullHalf", "ExpPos", "GaussDissolve", "Heartbeat", "ShDefault"]
+(SP_CRACK, SP_CRACKNORECON, SP_DISSOLVE, SP_NAIVEOUTLINE, SP_QUANTIZEFLATS, SP_QUANTIZELIGHT, SP_ROUGHNESSONLY,
+ SP_DEFAULT, SP_STENCIL, SP_WIREFRAME) = range(10)
+SPLAT_NAMES = ["Crack", "CrackNoRecon", "Dissolve", "NaiveOutline", "QuantizeFlats", "QuantizeLight",
+               "RoughnessOnly", "SplatDefault", "Stencil", "Wireframe"]
+# textures each shader samples (TextureManager names used in ShShader.cu / splatShader.cu)
+SH_TEXTURES = {SH_HEARTBEAT: ("Turbulence", "Craters"), SH_GAUSSDISSOLVE: ("Cracks", None)}
+SPLAT_TEXTURES = {SP_DISSOLVE: "Cracks", SP_CRACK: "Depth cracks", SP_CRACKNORECON: "Bulge"}
+# channels per TextureMode (texture.h), in r3dg_encode_texture_mode order
+MODE_CHANNELS = {0: 1, 1: 1, 2: 1, 9: 1, 10: 1, 3: 3, 6: 3, 7: 3, 8: 3, 4: 4, 5: 4}
+ADDR_WRAP, ADDR_CLAMP, ADDR_MIRROR, ADDR_BORDER = range(4)
+
+
+class OTex(ctypes.Structure):
+    _fields_ = [("texels", ctypes.c_void_p), ("W", ctypes.c_int), ("H", ctypes.c_int), ("wrap_u", ctypes.c_int),
+                ("wrap_v", ctypes.c_int), ("normalized", ctypes.c_int), ("linear", ctypes.c_int)]
+
+
+class Texture:
+    """AllocateTexture (texture.cu:86-233) for the oracle: pixels [H, W, C] padded to float4
+    texels (1 channel -> (x, 0, 0, 1), 3 channels -> alpha 1), bilinear sampling except LAB / HSV
+    (modes 7, 8: point sampling)."""
+
+    def __init__(self, pixels, mode=3, wrap_u=ADDR_WRAP, wrap_v=ADDR_WRAP, normalized=True):
+        C = MODE_CHANNELS[mode]
+        pix = np.asarray(pixels, F)
+        H, W = pix.shape[:2]
+        pix = pix.reshape(H, W, C)
+        t = np.zeros((H, W, 4), F)
+        t[..., 3] = 1.0
+        t[..., :C] = pix
+        self.texels = np.ascontiguousarray(t)
+        self.pixels = pix
+        self.mode, self.wrap = mode, (wrap_u, wrap_v)
+        self.normalized = bool(normalized)
+        self.desc = OTex(self.texels.ctypes.data, W, H, wrap_u, wrap_v, int(bool(normalized)),
+                         0 if mode in (7, 8) else 1)
+
+    def sample(self, xy):
+        """tex2D<float4> at each (x, y) row of xy [n, 2] -> [n, 4]."""
+        xy = _f(xy).reshape(-1, 2)
+        out = np.zeros((xy.shape[0], 4), F)
+        lib().oracle_tex_sample_batch(ctypes.byref(self.desc), ctypes.c_int(xy.shape[0]), _p(xy), _p(out))
+        return out
+
+
+def sh_shader(sid, idx, pos, scale, rot, opacity, sh, features=None, time=0.0, tex0=None, tex1=None):
+    """One SH shader over the splats idx, in place on the (float32, contiguous) arrays."""
+    idx = np.ascontiguousarray(idx, np.int32)
+    S = 0 if features is None else features.shape[1]
+    lib().oracle_sh_shader(ctypes.c_int(sid), ctypes.c_int(idx.size), _p(idx), ctypes.c_float(time), _p(pos),
+                           _p(scale), _p(rot), _p(opacity), _p(sh), ctypes.c_int(sh.shape[1]), _p(features),
+                           ctypes.c_int(S), ctypes.byref(tex0.desc) if tex0 else None,
+                           ctypes.byref(tex1.desc) if tex1 else None)
+
+
+def splat_shader(sid, idx, W, H, pos, means2D, depth_tex, view_inv, depths, rgb, conic_opacity, features, stencils,
+                 stencil_opacity, out_rgb, time=0.0, tex0=None):
+    """One splat shader over the splats idx, in place on conic_opacity / features / stencils /
+    stencil_opacity / out_rgb."""
+    idx = np.ascontiguousarray(idx, np.int32)
+    lib().oracle_splat_shader(ctypes.c_int(sid), ctypes.c_int(idx.size), _p(idx), ctypes.c_int(W), ctypes.c_int(H),
+                              ctypes.c_float(time), _p(pos), _p(means2D), _p(depth_tex), _p(_f(view_inv)), _p(depths),
+                              _p(rgb), _p(conic_opacity), _p(features), ctypes.c_int(features.shape[1]),
+                              _p(stencils), _p(stencil_opacity), _p(out_rgb),
+                              ctypes.byref(tex0.desc) if tex0 else None)
+
+
+# ---------------------------------------------------------------------------------------------
 # rasterizer
 # ---------------------------------------------------------------------------------------------
 def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales=None, rotations=None,
                       cov3D_precomp=None, colors_precomp=None, bg=(1.0, 1.0, 1.0), scale_modifier=1.0,
-                      compute_pseudo_normal=True):
-    """Full forward of rasterize_gaussians (rasterizer_impl.cu:213-529) with default shaders.
-    Returns a dict with the reference outputs (HWC) and the binning state."""
+                      compute_pseudo_normal=True, sh_shaders=None, splat_shaders=None, textures=None,
+                      error_texture=None, time=0.0):
+    """Full forward of rasterize_gaussians (rasterizer_impl.cu:213-529). Returns a dict with the
+    reference outputs (HWC) and the binning state.
+
+    Shaders (forward.cu:805-971): `sh_shaders` / `splat_shaders` are per-splat registry ids
+    (SH_* / SP_* below; None = the default shaders), `textures` maps names to `Texture`s and
+    `error_texture` stands in for missing names (TextureManager::GetTexture, texture.cu:298-314).
+    SH shaders edit working copies of the inputs before preprocessing; splat shaders run after
+    the intermediate depth / stencil pass and edit opacity, features and the shader colour."""
     L_ = lib()
     means3D = _f(means3D)
     P = means3D.shape[0]
@@ -81,6 +162,33 @@ def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales
     M = 0 if sh is None else sh.shape[1]
     scales, rotations, cov3D_precomp, colors_precomp = map(_f, (scales, rotations, cov3D_precomp, colors_precomp))
     opacity = _f(opacity).reshape(P)
+    sh_ids = None if sh_shaders is None else np.asarray(sh_shaders).reshape(-1)
+    sp_ids = None if splat_shaders is None else np.asarray(splat_shaders).reshape(-1)
+    sh_active = P > 0 and sh_ids is not None and bool((sh_ids != SH_DEFAULT).any())
+    splat_active = P > 0 and sp_ids is not None and bool((sp_ids != SP_DEFAULT).any())
+    originals = dict(means3D=means3D, scales=scales, rotations=rotations, sh=sh, features=features)
+    if sh_active or splat_active:  # working copies (rasterize_points.cu:117-122)
+        cp = lambda a: None if a is None else a.copy()  # noqa: E731
+        means3D, scales, rotations, opacity, sh, features = map(cp, (means3D, scales, rotations, opacity, sh,
+                                                                     features))
+
+    def tex(name):
+        if name is None:
+            return None
+        t = (textures or {}).get(name, error_texture)
+        if t is None:
+            raise ValueError(f"shader samples texture {name!r}: pass textures / error_texture")
+        return ctypes.byref(t.desc)
+
+    if sh_active:  # RunSHShaders (forward.cu:805-877)
+        for sid in np.unique(sh_ids):
+            if sid == SH_DEFAULT:
+                continue
+            idx = np.ascontiguousarray(np.nonzero(sh_ids == sid)[0], np.int32)
+            t0, t1 = SH_TEXTURES.get(int(sid), (None, None))
+            L_.oracle_sh_shader(ctypes.c_int(int(sid)), ctypes.c_int(idx.size), _p(idx), ctypes.c_float(time),
+                                _p(means3D), _p(scales), _p(rotations), _p(opacity), _p(sh), ctypes.c_int(M),
+                                _p(features), ctypes.c_int(S), tex(t0), tex(t1))
     view, proj, campos = _f(cam.view), _f(cam.proj), _f(cam.campos)
     radii = np.zeros(P, np.int32)
     means2D = np.zeros((P, 2), F)
@@ -110,6 +218,25 @@ def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales
     colors = colors_precomp if colors_precomp is not None else rgb
     bgv = np.asarray(bg, F)
     HW = H * W
+    stencil_img = np.zeros((H, W, 1), F)
+    shader_rgb = colors
+    if splat_active:
+        # RenderIntermediateTextures (forward.cu:271-383), then RunSplatShaders (forward.cu:907-971)
+        stencils = np.zeros(P, F)
+        stencil_opacity = np.ones(P, F)
+        depth_img = np.zeros((H, W, 1), F)
+        L_.oracle_render_intermediate(ctypes.c_int(W), ctypes.c_int(H), _p(ranges), _p(vals_s), _p(means2D),
+                                      _p(depths), _p(stencils), _p(conic), _p(stencil_opacity), _p(depth_img),
+                                      _p(stencil_img))
+        shader_rgb = np.zeros((P, 3), F)
+        vinv = _f(cam.view_inv)
+        for sid in np.unique(sp_ids):
+            idx = np.ascontiguousarray(np.nonzero(sp_ids == sid)[0], np.int32)
+            L_.oracle_splat_shader(ctypes.c_int(int(sid)), ctypes.c_int(idx.size), _p(idx), ctypes.c_int(W),
+                                   ctypes.c_int(H), ctypes.c_float(time), _p(means3D), _p(means2D), _p(depth_img),
+                                   _p(vinv), _p(depths), _p(colors), _p(conic), _p(features), ctypes.c_int(S),
+                                   _p(stencils), _p(stencil_opacity), _p(shader_rgb),
+                                   tex(SPLAT_TEXTURES.get(int(sid))))
     final_T = np.zeros(HW, F)
     n_contrib = np.zeros(HW, np.uint32)
     out_color = np.zeros((H, W, 3), F)
@@ -118,7 +245,7 @@ def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales
     out_depth = np.zeros((H, W, 1), F)
     out_feature = np.zeros((H, W, S), F)
     L_.oracle_render_forward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(S), _p(ranges), _p(vals_s),
-                             _p(means2D), _p(depths), _p(features), _p(colors), _p(colors), _p(conic), _p(bgv),
+                             _p(means2D), _p(depths), _p(features), _p(colors), _p(shader_rgb), _p(conic), _p(bgv),
                              _p(final_T), _p(n_contrib), _p(out_color), _p(out_opacity), _p(out_depth),
                              _p(out_feature), _p(out_shader))
     normal = np.zeros((H, W, 3), F)
@@ -129,14 +256,15 @@ def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales
                                      ctypes.c_float(fy), ctypes.c_float(cam.cx), ctypes.c_float(cam.cy),
                                      _p(out_opacity), _p(out_depth), _p(normal), _p(xyz))
     return dict(num_rendered=L, color=out_color, opacity=out_opacity, depth=out_depth,
-                stencil=np.zeros((H, W, 1), F), feature=out_feature, shader_color=out_shader, normal=normal,
+                stencil=stencil_img, feature=out_feature, shader_color=out_shader, normal=normal,
                 surface_xyz=xyz, radii=radii, n_contrib=n_contrib.reshape(H, W, 1), final_T=final_T,
                 keys=keys_s[:L], point_list=vals_s[:L], ranges=ranges, offsets=offsets, depths=depths,
                 means2D=means2D, conic_opacity=conic, rgb=rgb, clamped=clamped, cov3D=cov3D,
                 # inputs kept for the backward
-                _in=dict(means3D=means3D, features=features, sh=sh, degree=degree, scales=scales,
-                         rotations=rotations, cov3D_precomp=cov3D_precomp, colors_precomp=colors_precomp,
-                         scale_modifier=scale_modifier, bg=bgv, cam=cam))
+                # the backward reads the caller's tensors, not the shaded copies (rasterize_points.cu)
+                _in=dict(means3D=originals["means3D"], features=originals["features"], sh=originals["sh"],
+                         degree=degree, scales=originals["scales"], rotations=originals["rotations"],
+                         cov3D_precomp=cov3D_precomp, colors_precomp=colors_precomp, scale_modifier=scale_modifier, bg=bgv, cam=cam))
 
 
 def rasterize_backward(fwd, dL_dcolor, dL_dopacity, dL_ddepth, dL_dfeature, color_hwc=False, feature_native=False,

@@ -20,6 +20,7 @@
 
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
+#include "shaders.h"
 
 namespace r3dg {
 
@@ -221,6 +222,24 @@ static uint32_t higher_msb(uint32_t n) {
     return msb;
 }
 
+// InitializeStencil (rasterizer_impl.cu:203-209)
+__global__ void __launch_bounds__(256) init_stencil_kernel(int P, float* stencil, float* stencil_opacity) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    stencil[i] = 0.0f;
+    stencil_opacity[i] = 1.0f;
+}
+
+// Splat shaders edit conic_opacity.w after the render records were written: refresh the records'
+// opacity (the backward reads records; the reference's backward reads the edited geometry state).
+__global__ void __launch_bounds__(256) refresh_record_opacity_kernel(int P, const int* __restrict__ radii,
+                                                                     const float4* __restrict__ conic_opacity,
+                                                                     float4* __restrict__ records, int rec4) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P || radii[i] <= 0) return;
+    records[(size_t)i * rec4].w = conic_opacity[i].w;
+}
+
 // ---- shader registry (ShShader.cu:196-230, splatShader.cu:283-333, postProcessShader.cu:395-436) ----
 // Handles are opaque ids: (kind + 1) << 32 | index into the alphabetically ordered name list
 // (the reference's ShaderManager iterates a std::map, i.e. in name order).
@@ -362,21 +381,71 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     R3DG_REQUIRE((long long)H * W * (S > 3 ? S : 3) < (1ll << 31), "rasterize_gaussians: image too large");
     *num_rendered = 0;
 
-    // shaders: this build runs the default SH / splat shaders and no post-process passes
-    // (DESIGN.md "Scope"; the shader library is the next row of SURVEY.md §8f).
+    // shaders (forward.cu:805-971): SH shaders shade working copies of the inputs before
+    // preprocessing, splat shaders run after the intermediate depth/stencil pass
     ShaderManagerObj* shm = lookup_manager(s->sh_shader_manager);
     ShaderManagerObj* spm = lookup_manager(s->splat_shader_manager);
     R3DG_REQUIRE(s->sh_shader_manager == 0 || shm, "rasterize_gaussians: unknown SH shader manager handle");
     R3DG_REQUIRE(s->splat_shader_manager == 0 || spm, "rasterize_gaussians: unknown splat shader manager handle");
-    if ((shm && !shm->all_default) || (spm && !spm->all_default) || s->n_post_passes > 0) {
-        set_error("rasterize_gaussians: non-default SH/splat shaders and post-process passes are not in this "
-                  "build's scope yet (DESIGN.md 'Scope'); use default shaders (handle 0)");
+    R3DG_REQUIRE(!shm || shm->kind == R3DG_SHADER_SH, "rasterize_gaussians: h_shShaderManager is not an SH manager");
+    R3DG_REQUIRE(!spm || spm->kind == R3DG_SHADER_SPLAT,
+                 "rasterize_gaussians: h_splatShaderManager is not a splat manager");
+    if (s->n_post_passes > 0) {
+        set_error("rasterize_gaussians: post-process passes are not in this build's scope yet (SURVEY.md §8f "
+                  "rank 2); pass an empty list");
         return R3DG_ERR_UNSUPPORTED;
     }
+    const bool sh_active = P > 0 && shm && !shm->all_default;
+    const bool splat_active = P > 0 && spm && !spm->all_default;
+    const std::map<std::string, TexDesc>* tex_names = nullptr;
+    TexDesc tex_error{};
+    if (s->texture_manager)
+        R3DG_REQUIRE(lookup_texture_manager(s->texture_manager, &tex_names, &tex_error),
+                     "rasterize_gaussians: unknown texture manager handle");
+    // TextureManager::GetTexture (texture.cu:298-314): the error texture for a missing name
+    auto resolve = [&](const char* name, TexDesc* d) {
+        if (!name) return true;
+        if (!tex_names) return false;
+        auto it = tex_names->find(name);
+        *d = it == tex_names->end() ? tex_error : it->second;
+        return true;
+    };
+    auto check_shader = [&](int kind, int id) -> bool {
+        const bool feats = kind == R3DG_SHADER_SH ? sh_shader_needs_features(id) : splat_shader_needs_features(id);
+        if (feats && S < 21) {
+            set_error("rasterize_gaussians: shader " + shader_names(kind)[id] +
+                      " addresses the reference's 21-channel feature layout (ShShader.h/splatShader.h); S < 21");
+            return false;
+        }
+        TexDesc d{};
+        const char* t0 = kind == R3DG_SHADER_SH ? sh_shader_texture(id, 0) : splat_shader_texture(id);
+        const char* t1 = kind == R3DG_SHADER_SH ? sh_shader_texture(id, 1) : nullptr;
+        if (!resolve(t0, &d) || !resolve(t1, &d)) {
+            set_error("rasterize_gaussians: shader " + shader_names(kind)[id] + " samples textures; pass a "
+                      "texture manager (UploadTexturesToDevice)");
+            return false;
+        }
+        return true;
+    };
+    if (sh_active) {
+        R3DG_REQUIRE(g->scales && g->rotations && g->sh,
+                     "rasterize_gaussians: SH shaders need scales, rotations and SH coefficients");
+        for (int id = 0; id < (int)shm->counts.size(); ++id)
+            if (shm->counts[id] > 0 && id != kShDefault && !check_shader(R3DG_SHADER_SH, id)) return R3DG_ERR_ARG;
+    }
+    if (splat_active)
+        for (int id = 0; id < (int)spm->counts.size(); ++id)
+            if (spm->counts[id] > 0 && !check_shader(R3DG_SHADER_SPLAT, id)) return R3DG_ERR_ARG;
+    const bool work_copies = sh_active || splat_active;
 
     const int gx = (W + kTileX - 1) / kTileX, gy = (H + kTileY - 1) / kTileY;
     const int T = gx * gy;
-    void* geom_base = geom_alloc(geom_ctx, geom_state_bytes((size_t)P, S));
+    // working copies of the six inputs the shaders may edit (rasterize_points.cu:117-122), after
+    // the geometry state proper (the backward never reads them)
+    const size_t geom_bytes = geom_state_bytes((size_t)P, S);
+    const size_t M3 = (size_t)3 * (g->sh ? s->M : 0);
+    const size_t work_floats = work_copies ? (size_t)P * (3 + 3 + 4 + 1 + M3 + S) : 0;
+    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * work_floats);
     void* img_base = image_alloc(image_ctx, image_state_bytes(H, W));
     if (!geom_base || !img_base) {
         set_error("rasterize_gaussians: state allocation failed");
@@ -388,6 +457,49 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     const float focal_y = H / (2.0f * s->tan_fovy);
     const float focal_x = W / (2.0f * s->tan_fovx);
 
+    const float* means3D = g->means3D;
+    const float* scales = g->scales;
+    const float* rotations = g->rotations;
+    const float* opacity = g->opacity;
+    const float* shs = g->sh;
+    float* feats = const_cast<float*>(g->features);
+    if (work_copies) {
+        float* w = reinterpret_cast<float*>(static_cast<char*>(geom_base) + geom_bytes);
+        hipError_t ce = hipSuccess;
+        auto copy = [&](const float* src, size_t n) -> float* {
+            float* d = w;
+            w += n;
+            if (src && n && ce == hipSuccess) ce = hipMemcpyAsync(d, src, sizeof(float) * n, hipMemcpyDeviceToDevice, st);
+            return src ? d : nullptr;
+        };
+        means3D = copy(g->means3D, 3 * (size_t)P);
+        scales = copy(g->scales, 3 * (size_t)P);
+        rotations = copy(g->rotations, 4 * (size_t)P);
+        opacity = copy(g->opacity, (size_t)P);
+        shs = copy(g->sh, M3 * P);
+        feats = copy(g->features, (size_t)S * P);
+        R3DG_CHECK_HIP(ce);
+    }
+    if (P > 0) {
+        hipLaunchKernelGGL(init_stencil_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, geom.stencils,
+                           geom.stencil_opacity);
+        R3DG_CHECK_LAUNCH(s->debug, st);
+    }
+    if (sh_active) {  // RunSHShaders (forward.cu:805-877): one launch per non-empty bucket
+        for (int id = 0; id < (int)shm->counts.size(); ++id) {
+            if (shm->counts[id] == 0 || id == kShDefault) continue;
+            ShShaderArgs sa{};
+            sa.idx = shm->d_lists[id]; sa.n = shm->counts[id]; sa.time = s->time; sa.dt = s->dt;
+            sa.pos = const_cast<float*>(means3D); sa.scale = const_cast<float*>(scales);
+            sa.rot = const_cast<float*>(rotations); sa.opacity = const_cast<float*>(opacity);
+            sa.sh = const_cast<float*>(shs); sa.M = s->M; sa.features = feats; sa.S = S;
+            resolve(sh_shader_texture(id, 0), &sa.tex0);
+            resolve(sh_shader_texture(id, 1), &sa.tex1);
+            R3DG_CHECK_HIP(launch_sh_shader(id, sa, st));
+            R3DG_CHECK_LAUNCH(s->debug, st);
+        }
+    }
+
     int L = 0;
     if (P > 0) {
         PreprocessArgs pa{};
@@ -395,8 +507,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         pa.prefiltered = s->prefiltered;
         pa.focal_x = focal_x; pa.focal_y = focal_y; pa.tan_fovx = s->tan_fovx; pa.tan_fovy = s->tan_fovy;
         pa.scale_modifier = s->scale_modifier;
-        pa.means3D = g->means3D; pa.scales = g->scales; pa.rotations = g->rotations; pa.opacity = g->opacity;
-        pa.sh = g->sh; pa.cov3D_precomp = g->cov3D_precomp; pa.colors_precomp = g->colors_precomp;
+        pa.means3D = means3D; pa.scales = scales; pa.rotations = rotations; pa.opacity = opacity;
+        pa.sh = shs; pa.cov3D_precomp = g->cov3D_precomp; pa.colors_precomp = g->colors_precomp;
         pa.view = s->viewmatrix; pa.proj = s->projmatrix; pa.campos = s->campos;
         pa.radii = radii; pa.tiles_touched = geom.tiles_touched; pa.depth_keys = geom.depth_keys;
         pa.records = geom.records; pa.rec4 = record_f4(S); pa.S = S; pa.features = g->features;
@@ -467,8 +579,37 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
-    // stencil: default shaders give all-zero stencil values (InitializeStencil, rasterizer_impl.cu:203-209)
-    if (out->stencil) R3DG_CHECK_HIP(hipMemsetAsync(out->stencil, 0, sizeof(float) * (size_t)H * W, st));
+    if (splat_active) {
+        // RenderIntermediateTextures (forward.cu:271-383): depth + stencil images the splat shaders read
+        IntermediateArgs ia{};
+        ia.ranges = img.ranges; ia.point_list = bin.point_list; ia.means2D = geom.means2D;
+        ia.conic_opacity = geom.conic_opacity; ia.depths = geom.depths; ia.stencils = geom.stencils;
+        ia.stencil_opacity = geom.stencil_opacity; ia.W = W; ia.H = H; ia.grid_x = gx; ia.num_tiles = T;
+        ia.out_depth = out->depth; ia.out_stencil = out->stencil;
+        R3DG_REQUIRE(out->depth && out->stencil, "rasterize_gaussians: splat shaders need depth and stencil outputs");
+        hipLaunchKernelGGL(intermediate_kernel, dim3(padded_tile_grid(T)), dim3(kBlock), 0, st, ia);
+        R3DG_CHECK_LAUNCH(s->debug, st);
+        for (int id = 0; id < (int)spm->counts.size(); ++id) {  // RunSplatShaders (forward.cu:907-971)
+            if (spm->counts[id] == 0) continue;
+            SplatShaderArgs sp{};
+            sp.idx = spm->d_lists[id]; sp.n = spm->counts[id]; sp.W = W; sp.H = H; sp.time = s->time;
+            sp.dt = s->dt; sp.pos = means3D; sp.means2D = geom.means2D; sp.depth_tex = out->depth;
+            sp.stencil_tex = out->stencil; sp.viewmatrix_inv = s->viewmatrix_inv; sp.depths = geom.depths;
+            // the reference passes geomState.rgb even with precomputed colours (then uninitialised)
+            sp.rgb = g->colors_precomp ? g->colors_precomp : geom.rgb;
+            sp.conic_opacity = geom.conic_opacity; sp.features = feats; sp.S = S; sp.stencils = geom.stencils;
+            sp.stencil_opacity = geom.stencil_opacity; sp.out_rgb = geom.shader_rgb;
+            resolve(splat_shader_texture(id), &sp.tex0);
+            R3DG_CHECK_HIP(launch_splat_shader(id, sp, st));
+            R3DG_CHECK_LAUNCH(s->debug, st);
+        }
+        hipLaunchKernelGGL(refresh_record_opacity_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, radii,
+                           geom.conic_opacity, geom.records, record_f4(S));
+        R3DG_CHECK_LAUNCH(s->debug, st);
+    } else if (out->stencil) {
+        // default splat shaders leave every stencil value 0 (InitializeStencil, rasterizer_impl.cu:203-209)
+        R3DG_CHECK_HIP(hipMemsetAsync(out->stencil, 0, sizeof(float) * (size_t)H * W, st));
+    }
 
     RenderFwdArgs ra{};
     ra.records = geom.records;
@@ -478,8 +619,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     ra.conic_opacity = geom.conic_opacity;
     ra.depths = geom.depths;
     ra.colors = g->colors_precomp ? g->colors_precomp : geom.rgb;
-    ra.shader_colors = ra.colors;
-    ra.features = g->features;
+    ra.shader_colors = splat_active ? geom.shader_rgb : ra.colors;
+    ra.features = feats;
     ra.bg = s->bg;
     ra.S = S; ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = T; ra.cull = 1;
     ra.tile_order = nullptr;  // forward: XCD-aware spatial order (measured faster: L2 locality)
@@ -495,7 +636,7 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     if (const char* e = getenv("R3DG_NO_CULL")) ra.cull = (e[0] == '0');
     {
         ProfScope ps(R3DG_PROF_RENDER_FWD, st);
-        R3DG_CHECK_HIP(launch_render_forward(ra, false, st));
+        R3DG_CHECK_HIP(launch_render_forward(ra, splat_active, st));
     }
     R3DG_CHECK_LAUNCH(s->debug, st);
 

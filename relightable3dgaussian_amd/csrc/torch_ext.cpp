@@ -419,14 +419,39 @@ std::tuple<std::vector<int64_t>, std::vector<int64_t>> shader_manager_info(int64
     return {h, std::vector<int64_t>(c.begin(), c.end())};
 }
 
-int64_t allocate_texture(const std::map<std::string, torch::Tensor>&) {
-    throw std::runtime_error(
-        "AllocateTexture: the texture manager serves only the non-default shader library, which is the next row "
-        "of this build's scope (DESIGN.md 'Scope'); default shaders need no textures");
+// AllocateTexture (texture.cu:86-101): the dict textureImport.py builds -- pixelData [H, W, C]
+// float, height, width, encoding_mode, wrap_modes [2], normalizedCoords (CPU int32 tensors)
+int64_t allocate_texture(const std::map<std::string, torch::Tensor>& d) {
+    auto scalar = [&](const char* k, int i = 0) {
+        auto it = d.find(k);
+        if (it == d.end()) throw std::runtime_error(std::string("AllocateTexture: missing '") + k + "'");
+        return it->second.to(torch::kCPU).to(torch::kInt64).contiguous().data_ptr<int64_t>()[i];
+    };
+    auto it = d.find("pixelData");
+    if (it == d.end()) throw std::runtime_error("AllocateTexture: missing 'pixelData'");
+    torch::Tensor pix = it->second.to(torch::kFloat32).contiguous();
+    if (!pix.is_cuda()) pix = pix.cuda();
+    const int H = (int)scalar("height"), W = (int)scalar("width"), mode = (int)scalar("encoding_mode");
+    const int C = pix.numel() / std::max<int64_t>((int64_t)H * W, 1);
+    if ((int64_t)C * H * W != pix.numel()) throw std::runtime_error("AllocateTexture: pixelData is not [H, W, C]");
+    c10::OptionalDeviceGuard guard(pix.device());
+    int64_t h = 0;
+    check(r3dg_texture_create(pix.data_ptr<float>(), W, H, mode, (int)scalar("wrap_modes", 0),
+                              (int)scalar("wrap_modes", 1), (int)scalar("normalizedCoords"), &h,
+                              c10::hip::getCurrentHIPStream(pix.device().index()).stream()),
+          "AllocateTexture");
+    return h;
 }
-int64_t upload_textures(const std::vector<std::string>&, const std::vector<int64_t>&, int64_t) {
-    throw std::runtime_error(
-        "UploadTexturesToDevice: the texture manager is not in this build's scope yet (DESIGN.md 'Scope')");
+// UploadTexturesToDevice (texture.cu:237-246)
+int64_t upload_textures(const std::vector<std::string>& names, const std::vector<int64_t>& textures,
+                        int64_t error_texture) {
+    if (names.size() != textures.size()) throw std::runtime_error("UploadTexturesToDevice: names/textures mismatch");
+    std::vector<const char*> cn;
+    for (const auto& n : names) cn.push_back(n.c_str());
+    int64_t h = 0;
+    check(r3dg_texture_manager_create((int)names.size(), cn.data(), textures.data(), error_texture, &h),
+          "UploadTexturesToDevice");
+    return h;
 }
 
 // parity / debug accessor: views of the sorted keys, point list, tile ranges and per-Gaussian state
