@@ -245,7 +245,7 @@ def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales
     out_depth = np.zeros((H, W, 1), F)
     out_feature = np.zeros((H, W, S), F)
     L_.oracle_render_forward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(S), _p(ranges), _p(vals_s),
-                             _p(means2D), _p(depths), _p(features), _p(colors), _p(shader_rgb), _p(conic), _p(bgv),
+                             _p(means2D), _p(depths), _p(features), _p(shader_rgb), _p(colors), _p(conic), _p(bgv),
                              _p(final_T), _p(n_contrib), _p(out_color), _p(out_opacity), _p(out_depth),
                              _p(out_feature), _p(out_shader))
     normal = np.zeros((H, W, 3), F)

@@ -202,6 +202,19 @@ def test_default_managers_are_the_default_path():
         np.testing.assert_array_equal(a[k], c[k], err_msg=k)
 
 
+def test_splat_shader_colour_goes_to_shader_image_only():
+    """Splat shaders write geomState.shader_rgb: out_color keeps the SH colour, out_shader_color
+    blends the shaded one (FORWARD::render arguments, rasterizer_impl.cu:436-456)."""
+    scene, cam = shader_scene(P=1500, seed=9)
+    kw = dict(sh=scene.sh, scales=scene.scales, rotations=scene.rotations)
+    a = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features, **kw)
+    b = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features, **kw,
+                                 splat_shaders=np.full(scene.P, oracle.SP_WIREFRAME))
+    for k in ["color", "opacity", "depth", "feature"]:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert np.abs(a["shader_color"] - b["shader_color"]).max() > 0.1
+
+
 def test_roughness_only_and_quantize_light():
     scene, cam = shader_scene(P=1000, seed=8)
     P = scene.P
