@@ -77,7 +77,10 @@ typedef struct r3dg_raster_settings {
     int64_t sh_shader_manager;    /* handle from r3dg_preprocess_model, 0 = all ShDefault */
     int64_t splat_shader_manager; /* handle from r3dg_preprocess_model, 0 = all SplatDefault */
     int64_t texture_manager;      /* 0 = none */
-    const int64_t* post_passes;   /* host array of post-process pass handles */
+    const int64_t* post_passes;   /* host array of post-process pass handles, run in order after the
+                                     blend (FORWARD::RunPostProcessShaders, forward.cu:973-1047);
+                                     a non-empty list re-renders depth + stencil first
+                                     (rasterizer_impl.cu:485-502) */
     int n_post_passes;
 } r3dg_raster_settings;
 

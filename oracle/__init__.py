@@ -73,6 +73,10 @@ SH_NAMES = ["CullHalf", "ExpPos", "GaussDissolve", "Heartbeat", "ShDefault"]
  SP_DEFAULT, SP_STENCIL, SP_WIREFRAME) = range(10)
 SPLAT_NAMES = ["Crack", "CrackNoRecon", "Dissolve", "NaiveOutline", "QuantizeFlats", "QuantizeLight",
                "RoughnessOnly", "SplatDefault", "Stencil", "Wireframe"]
+(PP_BLURLIGHTING, PP_CRACKRECON, PP_INVERT, PP_OUTLINE, PP_QUANTIZELIGHTING, PP_SOBEL, PP_DEFAULT,
+ PP_TEXTUREDSHADOWS, PP_TOON) = range(9)
+POST_NAMES = ["BlurLighting", "CrackReconstriction", "Invert", "Outline", "QuantizeLighting", "SobelFilter",
+              "SplatDefault", "TexturedShadows", "ToonShader"]
 # textures each shader samples (TextureManager names used in ShShader.cu / splatShader.cu)
 SH_TEXTURES = {SH_HEARTBEAT: ("Turbulence", "Craters"), SH_GAUSSDISSOLVE: ("Cracks", None)}
 SPLAT_TEXTURES = {SP_DISSOLVE: "Cracks", SP_CRACK: "Depth cracks", SP_CRACKNORECON: "Bulge"}
@@ -142,7 +146,7 @@ def splat_shader(sid, idx, W, H, pos, means2D, depth_tex, view_inv, depths, rgb,
 def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales=None, rotations=None,
                       cov3D_precomp=None, colors_precomp=None, bg=(1.0, 1.0, 1.0), scale_modifier=1.0,
                       compute_pseudo_normal=True, sh_shaders=None, splat_shaders=None, textures=None,
-                      error_texture=None, time=0.0):
+                      error_texture=None, time=0.0, post_passes=None):
     """Full forward of rasterize_gaussians (rasterizer_impl.cu:213-529). Returns a dict with the
     reference outputs (HWC) and the binning state.
 
@@ -150,7 +154,9 @@ def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales
     (SH_* / SP_* below; None = the default shaders), `textures` maps names to `Texture`s and
     `error_texture` stands in for missing names (TextureManager::GetTexture, texture.cu:298-314).
     SH shaders edit working copies of the inputs before preprocessing; splat shaders run after
-    the intermediate depth / stencil pass and edit opacity, features and the shader colour."""
+    the intermediate depth / stencil pass and edit opacity, features and the shader colour.
+    `post_passes` (PP_* ids, in order) re-render depth + stencil and run the screen passes
+    (rasterizer_impl.cu:485-529)."""
     L_ = lib()
     means3D = _f(means3D)
     P = means3D.shape[0]
@@ -220,10 +226,10 @@ def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales
     HW = H * W
     stencil_img = np.zeros((H, W, 1), F)
     shader_rgb = colors
+    stencils = np.zeros(P, F)          # InitializeStencil (rasterizer_impl.cu:203-209)
+    stencil_opacity = np.ones(P, F)
     if splat_active:
         # RenderIntermediateTextures (forward.cu:271-383), then RunSplatShaders (forward.cu:907-971)
-        stencils = np.zeros(P, F)
-        stencil_opacity = np.ones(P, F)
         depth_img = np.zeros((H, W, 1), F)
         L_.oracle_render_intermediate(ctypes.c_int(W), ctypes.c_int(H), _p(ranges), _p(vals_s), _p(means2D),
                                       _p(depths), _p(stencils), _p(conic), _p(stencil_opacity), _p(depth_img),
@@ -255,6 +261,17 @@ def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales
         L_.oracle_surface_xyz_normal(ctypes.c_int(W), ctypes.c_int(H), _p(view), ctypes.c_float(fx),
                                      ctypes.c_float(fy), ctypes.c_float(cam.cx), ctypes.c_float(cam.cy),
                                      _p(out_opacity), _p(out_depth), _p(normal), _p(xyz))
+    if post_passes is not None and len(post_passes) > 0:
+        # rasterizer_impl.cu:485-529: depth + stencil rendered again, then RunPostProcessShaders
+        L_.oracle_render_intermediate(ctypes.c_int(W), ctypes.c_int(H), _p(ranges), _p(vals_s), _p(means2D),
+                                      _p(depths), _p(stencils), _p(conic), _p(stencil_opacity), _p(out_depth),
+                                      _p(stencil_img))
+        ids = np.ascontiguousarray(post_passes, np.int32)
+        needs_shadow = bool(np.isin(ids, [PP_TEXTUREDSHADOWS, PP_TOON]).any())
+        L_.oracle_post_passes(_p(ids), ctypes.c_int(ids.size), ctypes.c_int(W), ctypes.c_int(H), _p(view),
+                              _p(out_color), _p(out_opacity), _p(out_depth), _p(stencil_img), _p(xyz), _p(normal),
+                              _p(out_feature) if S == 21 else None, _p(out_shader),
+                              tex("shadow") if needs_shadow else None)
     return dict(num_rendered=L, color=out_color, opacity=out_opacity, depth=out_depth,
                 stencil=stencil_img, feature=out_feature, shader_color=out_shader, normal=normal,
                 surface_xyz=xyz, radii=radii, n_contrib=n_contrib.reshape(H, W, 1), final_T=final_T,

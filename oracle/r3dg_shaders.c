@@ -10,10 +10,13 @@
  * bool overload of mix is a select. Parity note: the reference has no fixtures for shaders or
  * textures, and the hardware rounding of CUDA's fixed-point texture weights is not published
  * (round-to-nearest assumed): shader parity is pinned only by this restatement.
+ * Post-process passes: postProcessShader.cu:13-374 with RunPostProcessShaders' double buffer
+ * (forward.cu:973-1047) restated literally; helpers from shaderUtils.cu:6-161.
  * Build: oracle/Makefile (-ffp-contract=off).
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #ifndef M_PI
@@ -263,4 +266,218 @@ void oracle_splat_shader(int id, int n, const int* idx, int W, int H, float time
             memcpy(out, F + 9, 3 * sizeof(float));
         }
     }
+}
+
+/* ---- post-process passes ------------------------------------------------------------------ */
+enum {
+    PP_BLURLIGHTING = 0, PP_CRACKRECON = 1, PP_INVERT = 2, PP_OUTLINE = 3, PP_QUANTIZELIGHTING = 4,
+    PP_SOBEL = 5, PP_DEFAULT = 6, PP_TEXTUREDSHADOWS = 7, PP_TOON = 8
+};
+
+static void rgb_to_hsv(const float* c, float* hsv) /* shaderUtils.cu:6-37 */
+{
+    float mx = fmaxf(c[0], fmaxf(c[1], c[2])), mn = fminf(c[0], fminf(c[1], c[2]));
+    float diff = mx - mn;
+    hsv[2] = mx;
+    if (hsv[2] == 0.0f) {
+        hsv[0] = hsv[1] = 0.0f;
+    } else {
+        hsv[1] = diff / hsv[2];
+        if (diff < 0.001f) {
+            hsv[0] = 0.0f;
+        } else if (mx == c[0]) {
+            hsv[0] = (c[1] - c[2]) / diff / 6;
+            if (hsv[0] < 0.0f) hsv[0] += 1.0f;
+        } else if (mx == c[1]) {
+            hsv[0] = (2 + (c[2] - c[0]) / diff) / 6;
+        } else {
+            hsv[0] = (4 + (c[0] - c[1]) / diff) / 6;
+        }
+    }
+}
+
+static void hsv_to_rgb(const float* hsv, float* o) /* shaderUtils.cu:41-82 */
+{
+    float h = hsv[0], s = hsv[1], v = hsv[2];
+    float f = h * 6, hi = floorf(f);
+    f = f - hi;
+    float p = v * (1 - s), q = v * (1 - s * f), t = v * (1 - s * (1 - f));
+    float r, g, b;
+    if (hi == 0.0f || hi == 6.0f) { r = v; g = t; b = p; }
+    else if (hi == 1.0f) { r = q; g = v; b = p; }
+    else if (hi == 2.0f) { r = p; g = v; b = t; }
+    else if (hi == 3.0f) { r = p; g = q; b = v; }
+    else if (hi == 4.0f) { r = t; g = p; b = v; }
+    else { r = v; g = p; b = q; }
+    o[0] = r; o[1] = g; o[2] = b;
+}
+
+static const float kBlend[5][5] = {{0.009375f, 0.01875f, 0.028125f, 0.01875f, 0.009375f},
+                                   {0.01875f, 0.0375f, 0.045f, 0.0375f, 0.01875f},
+                                   {0.028125f, 0.045f, 0.3f, 0.045f, 0.028125f},
+                                   {0.01875f, 0.0375f, 0.045f, 0.0375f, 0.01875f},
+                                   {0.009375f, 0.01875f, 0.028125f, 0.01875f, 0.009375f}};
+
+/* PostProcessShaderBuffer views (postProcessShader.cu:13-105) */
+typedef struct {
+    float *features, *metallic, *incident, *base, *opacity, *depth, *stencil, *xyz, *normal, *shader, *sh;
+} pp_buf;
+
+static pp_buf pp_views(float* features, float* opacity, float* depth, float* stencil, float* xyz, float* normal,
+                       float* shader, float* sh, long HW)
+{
+    pp_buf b;
+    b.features = features;
+    b.metallic = features ? features + HW : NULL;
+    b.base = features ? features + 9 * HW : NULL;
+    b.incident = features ? features + 12 * HW : NULL;
+    b.opacity = opacity; b.depth = depth; b.stencil = stencil; b.xyz = xyz; b.normal = normal;
+    b.shader = shader; b.sh = sh;
+    return b;
+}
+
+static void pp_color_correction(const pp_buf* in, const pp_buf* out, long p) /* :276-289 */
+{
+    float hsv[3], color[3];
+    rgb_to_hsv(in->base + 3 * p, hsv);
+    hsv[0] = roundf(hsv[0] * 24) / 24;
+    hsv_to_rgb(hsv, color);
+    float intensity = in->incident[3 * p];
+    float reduced = sat(intensity + 0.25f);
+    for (int c = 0; c < 3; ++c) out->shader[3 * p + c] = color[c] * reduced;
+}
+
+static void pp_textured_shadows(const pp_buf* in, const pp_buf* out, long p, int x, int y, int W, int H,
+                                const otex* shadow) /* :238-274 */
+{
+    if (in->stencil[p] < 0.01f) {
+        for (int c = 0; c < 3; ++c) out->shader[3 * p + c] = 1.0f;
+        return;
+    }
+    float uvScale = 10;
+    float u = (float)x / (float)W * uvScale, v = (float)y / (float)H * uvScale;
+    float t[4];
+    oracle_tex_sample(shadow, u, v, t);
+    float lightShadow = 1 - t[0], mediumShadow = 1 - t[2], heavyShadow = 1 - t[1];
+    const float* L = in->incident + 3 * p;
+    float m = L[1] > L[2] ? L[1] : L[2]; /* __max */
+    float intensity = L[0] > m ? L[0] : m;
+    intensity = roundf(intensity * 4);
+    heavyShadow = sat(heavyShadow + intensity);
+    intensity = 0 > intensity - 1.0f ? 0 : intensity - 1.0f;
+    mediumShadow = sat(mediumShadow + intensity);
+    intensity = 0 > intensity - 1.0f ? 0 : intensity - 1.0f;
+    lightShadow = sat(lightShadow + intensity);
+    for (int c = 0; c < 3; ++c) out->shader[3 * p + c] = out->shader[3 * p + c] * lightShadow * mediumShadow * heavyShadow;
+}
+
+static void pp_sobel(const pp_buf* in, const pp_buf* out, long p, int W) /* :304-331 */
+{
+    const float SH[3][3] = {{-1, 0, 1}, {-2, 0, 2}, {-1, 0, 1}};
+    const float SV[3][3] = {{-1, -2, -1}, {0, 0, 0}, {1, 2, 1}};
+    float outlineStrength = 2, hori = 0, vert = 0;
+    for (int x = -1; x < 2; x++)
+        for (int y = -1; y < 2; y++) {
+            long sp = p + x + (long)y * W;
+            float d = in->depth[sp]; /* unclamped: neighbouring planes of the input buffer */
+            hori += SH[x + 1][y + 1] * d * outlineStrength;
+            vert += SV[x + 1][y + 1] * d * outlineStrength;
+        }
+    int depthChange = (int)sqrtf(powf(hori, 2) + powf(vert, 2));
+    float k = sat((float)(1 - abs(depthChange)));
+    for (int c = 0; c < 3; ++c) out->shader[3 * p + c] = out->shader[3 * p + c] * k;
+}
+
+static void pp_run(int id, const pp_buf* in, const pp_buf* out, long p, int x, int y, int W, int H,
+                   const float* view, const otex* shadow)
+{
+    (void)view;
+    long HW = (long)W * H;
+    float* sc = out->shader + 3 * p;
+    switch (id) {
+    case PP_INVERT: /* :187-189 */
+        for (int c = 0; c < 3; ++c) sc[c] = 1 - in->shader[3 * p + c];
+        break;
+    case PP_OUTLINE: { /* :212-232 (every sample tests in.pixel itself) */
+        long idx = p;
+        int inside = !(idx < 0 || idx > HW) && in->stencil[idx] >= 0.9f;
+        int outside = !inside, near = 0;
+        for (float radius = 1; radius < 5 + 1; radius++)
+            for (float direction = 0; direction <= 1; direction += 1.0f / (float)5) near |= inside;
+        float o = (float)(outside && near);
+        const float red[3] = {1, 0, 0};
+        for (int c = 0; c < 3; ++c) sc[c] = in->base[3 * p + c] * (1.0f - o) + red[c] * o;
+        break;
+    }
+    case PP_CRACKRECON: { /* :234-261 */
+        float mask = in->stencil[p] * in->metallic[p];
+        if (mask <= 0.01f) break;
+        const float* n = in->normal + 3 * p;
+        float ld[3] = {0, -0.2f, 1};
+        float inv = 1.0f / sqrtf(dot3(ld, ld));
+        for (int c = 0; c < 3; ++c) ld[c] = ld[c] * inv;
+        float internal[3] = {0.83f, 0.64f, 0.2f};
+        float k = sat(sat(dot3(ld, n) * 0.1f) + 0.9f);
+        for (int c = 0; c < 3; ++c) {
+            internal[c] *= k;
+            sc[c] = internal[c] * mask + in->shader[3 * p + c] * (1 - mask);
+        }
+        break;
+    }
+    case PP_TEXTUREDSHADOWS: pp_textured_shadows(in, out, p, x, y, W, H, shadow); break;
+    case PP_QUANTIZELIGHTING: { /* :291-297 */
+        const float* L = in->incident + 3 * p;
+        float white = fmaxf(L[0], fmaxf(L[1], L[2]));
+        float q = roundf(white * 4) / 4;
+        for (int c = 0; c < 3; ++c) out->incident[3 * p + c] = q;
+        break;
+    }
+    case PP_BLURLIGHTING: { /* :299-309, GaussianBlur shaderUtils.cu:104-123 */
+        const float* pix = in->incident + 3 * p;
+        if (pix[0] == 0 && pix[1] == 0 && pix[2] == 0) break;
+        float acc[3] = {0, 0, 0};
+        for (int dx = -2; dx < 3; dx++)
+            for (int dy = -2; dy < 3; dy++) {
+                long sp = p + dx + (long)dy * W;
+                sp = sp < 0 ? 0 : (sp > HW - 1 ? HW - 1 : sp);
+                for (int c = 0; c < 3; ++c) acc[c] += kBlend[dx + 2][dy + 2] * in->incident[3 * sp + c];
+            }
+        for (int c = 0; c < 3; ++c) out->incident[3 * p + c] = acc[c];
+        break;
+    }
+    case PP_SOBEL: pp_sobel(in, out, p, W); break;
+    case PP_TOON: /* :333-337 */
+        pp_color_correction(in, out, p);
+        pp_textured_shadows(in, out, p, x, y, W, H, shadow);
+        pp_sobel(in, out, p, W);
+        break;
+    default: break; /* DefaultPostProcess */
+    }
+}
+
+/* RunPostProcessShaders (forward.cu:973-1047). `features` is out_feature in the reference's
+ * 21-channel block layout (NULL when S != 21: the feature planes of the copy stay zero). The
+ * thread -> pixel mapping is x = idx % W, y = idx / W (the reference divides by H, which only
+ * agrees for square images). */
+void oracle_post_passes(const int* ids, int n, int W, int H, const float* view, float* color, float* opacity,
+                        float* depth, float* stencil, float* xyz, float* normal, float* features, float* shader,
+                        const otex* shadow)
+{
+    long HW = (long)W * H;
+    if (n <= 0 || HW == 0) return;
+    /* CreateDeepBuffer: one allocation, 21 feature planes + 15 scene planes */
+    float* buf = (float*)calloc((size_t)36 * HW, sizeof(float));
+    pp_buf out = pp_views(features, opacity, depth, stencil, xyz, normal, shader, color, HW);
+    pp_buf in = pp_views(buf, buf + 21 * HW, buf + 22 * HW, buf + 23 * HW, buf + 24 * HW, buf + 27 * HW,
+                         buf + 30 * HW, buf + 33 * HW, HW);
+    float* planes_out[8] = {features, opacity, depth, stencil, xyz, normal, shader, color};
+    const long sizes[8] = {21 * HW, HW, HW, HW, 3 * HW, 3 * HW, 3 * HW, 3 * HW};
+    const long offs[8] = {0, 21 * HW, 22 * HW, 23 * HW, 24 * HW, 27 * HW, 30 * HW, 33 * HW};
+    for (int i = 0; i < n; ++i) {
+        /* DeepCopy (before the first pass, then between passes) */
+        for (int k = 0; k < 8; ++k)
+            if (planes_out[k]) memcpy(buf + offs[k], planes_out[k], sizeof(float) * (size_t)sizes[k]);
+        for (long p = 0; p < HW; ++p) pp_run(ids[i], &in, &out, p, (int)(p % W), (int)(p / W), W, H, view, shadow);
+    }
+    free(buf);
 }

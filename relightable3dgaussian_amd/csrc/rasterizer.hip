@@ -390,11 +390,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     R3DG_REQUIRE(!shm || shm->kind == R3DG_SHADER_SH, "rasterize_gaussians: h_shShaderManager is not an SH manager");
     R3DG_REQUIRE(!spm || spm->kind == R3DG_SHADER_SPLAT,
                  "rasterize_gaussians: h_splatShaderManager is not a splat manager");
-    if (s->n_post_passes > 0) {
-        set_error("rasterize_gaussians: post-process passes are not in this build's scope yet (SURVEY.md §8f "
-                  "rank 2); pass an empty list");
-        return R3DG_ERR_UNSUPPORTED;
-    }
+    R3DG_REQUIRE(s->n_post_passes >= 0 && (s->n_post_passes == 0 || s->post_passes),
+                 "rasterize_gaussians: invalid post-process pass list");
     const bool sh_active = P > 0 && shm && !shm->all_default;
     const bool splat_active = P > 0 && spm && !spm->all_default;
     const std::map<std::string, TexDesc>* tex_names = nullptr;
@@ -437,6 +434,32 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         for (int id = 0; id < (int)spm->counts.size(); ++id)
             if (spm->counts[id] > 0 && !check_shader(R3DG_SHADER_SPLAT, id)) return R3DG_ERR_ARG;
     const bool work_copies = sh_active || splat_active;
+    // post-process passes (rasterizer_impl.cu:485-529): registry ids in list order
+    std::vector<int> post_ids;
+    bool post_blur = false;
+    TexDesc shadow_tex{};
+    for (int i = 0; i < s->n_post_passes; ++i) {
+        const int64_t h = s->post_passes[i];
+        const int id = handle_index(h);
+        R3DG_REQUIRE(handle_kind(h) == R3DG_SHADER_POST && id >= 0 && id < (int)shader_names(R3DG_SHADER_POST).size(),
+                     "rasterize_gaussians: unknown post-process pass handle (GetPostProcessShaderAddressMap)");
+        const std::string& name = shader_names(R3DG_SHADER_POST)[id];
+        if (post_pass_needs_features(id) && S != 21) {
+            set_error("rasterize_gaussians: post-process pass " + name +
+                      " reads the reference's 21-channel feature image (postProcessShader.cu:17-28); S != 21");
+            return R3DG_ERR_ARG;
+        }
+        if (post_pass_needs_shadow(id) && !resolve("shadow", &shadow_tex)) {
+            set_error("rasterize_gaussians: post-process pass " + name +
+                      " samples the \"shadow\" texture; pass a texture manager (UploadTexturesToDevice)");
+            return R3DG_ERR_ARG;
+        }
+        post_blur = post_blur || id == kPpBlurLighting;
+        post_ids.push_back(id);
+    }
+    R3DG_REQUIRE(post_ids.empty() || (out->color && out->opacity && out->depth && out->stencil && out->shader_color &&
+                                      out->normal && out->surface_xyz && (S == 0 || out->feature)),
+                 "rasterize_gaussians: post-process passes need every image output");
 
     const int gx = (W + kTileX - 1) / kTileX, gy = (H + kTileY - 1) / kTileY;
     const int T = gx * gy;
@@ -445,7 +468,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     const size_t geom_bytes = geom_state_bytes((size_t)P, S);
     const size_t M3 = (size_t)3 * (g->sh ? s->M : 0);
     const size_t work_floats = work_copies ? (size_t)P * (3 + 3 + 4 + 1 + M3 + S) : 0;
-    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * work_floats);
+    const size_t post_floats = post_blur ? (size_t)3 * H * W : 0;  // BlurLighting's incident-light snapshot
+    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * (work_floats + post_floats));
     void* img_base = image_alloc(image_ctx, image_state_bytes(H, W));
     if (!geom_base || !img_base) {
         set_error("rasterize_gaussians: state allocation failed");
@@ -579,13 +603,14 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
+    // RenderIntermediateTextures (forward.cu:271-383): depth + stencil images
+    IntermediateArgs ia{};
+    ia.ranges = img.ranges; ia.point_list = bin.point_list; ia.means2D = geom.means2D;
+    ia.conic_opacity = geom.conic_opacity; ia.depths = geom.depths; ia.stencils = geom.stencils;
+    ia.stencil_opacity = geom.stencil_opacity; ia.W = W; ia.H = H; ia.grid_x = gx; ia.num_tiles = T;
+    ia.out_depth = out->depth; ia.out_stencil = out->stencil;
     if (splat_active) {
-        // RenderIntermediateTextures (forward.cu:271-383): depth + stencil images the splat shaders read
-        IntermediateArgs ia{};
-        ia.ranges = img.ranges; ia.point_list = bin.point_list; ia.means2D = geom.means2D;
-        ia.conic_opacity = geom.conic_opacity; ia.depths = geom.depths; ia.stencils = geom.stencils;
-        ia.stencil_opacity = geom.stencil_opacity; ia.W = W; ia.H = H; ia.grid_x = gx; ia.num_tiles = T;
-        ia.out_depth = out->depth; ia.out_stencil = out->stencil;
+        // the splat shaders read the intermediate depth / stencil images
         R3DG_REQUIRE(out->depth && out->stencil, "rasterize_gaussians: splat shaders need depth and stencil outputs");
         hipLaunchKernelGGL(intermediate_kernel, dim3(padded_tile_grid(T)), dim3(kBlock), 0, st, ia);
         R3DG_CHECK_LAUNCH(s->debug, st);
@@ -651,6 +676,21 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         if (out->normal) R3DG_CHECK_HIP(hipMemsetAsync(out->normal, 0, sizeof(float) * 3 * (size_t)H * W, st));
         if (out->surface_xyz)
             R3DG_CHECK_HIP(hipMemsetAsync(out->surface_xyz, 0, sizeof(float) * 3 * (size_t)H * W, st));
+    }
+    if (!post_ids.empty()) {
+        // rasterizer_impl.cu:485-529: depth and stencil are rendered again (now with the splat
+        // shaders' stencils) and replace the blended depth, then the passes run in list order
+        hipLaunchKernelGGL(intermediate_kernel, dim3(padded_tile_grid(T)), dim3(kBlock), 0, st, ia);
+        R3DG_CHECK_LAUNCH(s->debug, st);
+        PostArgs pp{};
+        pp.W = W; pp.H = H; pp.sh_color = out->color; pp.opacity = out->opacity; pp.depth = out->depth;
+        pp.stencil = out->stencil; pp.surface_xyz = out->surface_xyz; pp.pseudonormal = out->normal;
+        pp.shader_color = out->shader_color; pp.features = S == 21 ? out->feature : nullptr;
+        pp.shadow = shadow_tex;
+        float* scratch = post_blur ? reinterpret_cast<float*>(static_cast<char*>(geom_base) + geom_bytes) + work_floats
+                                   : nullptr;
+        R3DG_CHECK_HIP(launch_post_passes(post_ids.data(), (int)post_ids.size(), pp, scratch, st));
+        R3DG_CHECK_LAUNCH(s->debug, st);
     }
     *num_rendered = L;
     return R3DG_OK;

@@ -116,7 +116,39 @@ struct SplatShaderArgs {
     TexDesc tex0;
 };
 
+// Post-process passes (postProcessShader.cu:177-374), registry ids in name order
+enum PostShaderId {
+    kPpBlurLighting = 0, kPpCrackReconstruction = 1, kPpInvert = 2, kPpOutline = 3, kPpQuantizeLighting = 4,
+    kPpSobelFilter = 5, kPpDefault = 6, kPpTexturedShadows = 7, kPpToon = 8
+};
+constexpr int kMaxFusedPasses = 16;
+
+// Screen buffers the passes read and write (the reference's PostProcessShaderBuffer views,
+// postProcessShader.cu:13-39). Writes go to the live outputs as in the reference; the only pass
+// that reads neighbours of a channel a pass writes (BlurLighting: incident light) reads a
+// snapshot of that block instead of the reference's full 36-channel double buffer.
+struct PostArgs {
+    int W, H;
+    const float* sh_color;      // out_color [H,W,3]
+    const float* opacity;       // out_opacity [H,W]
+    const float* depth;         // intermediate depth, re-rendered before the passes
+    const float* stencil;       // intermediate stencil
+    const float* surface_xyz;   // [H,W,3]
+    const float* pseudonormal;  // [H,W,3]
+    float* shader_color;        // [H,W,3]
+    float* features;            // out_feature in the reference's 21-channel block layout, or null
+    const float* incident_in;   // BlurLighting: snapshot of the incident-light block [H*W,3]
+    TexDesc shadow;             // "shadow" (TexturedShadows / ToonShader)
+    int n_pass;
+    int pass[kMaxFusedPasses];
+};
+
 hipError_t launch_sh_shader(int id, const ShShaderArgs& a, hipStream_t st);
+// Runs the passes ids[0..n) in order. Runs of pixel-local passes fuse into one launch; a
+// BlurLighting pass snapshots the incident-light block into scratch (3*W*H floats) first.
+hipError_t launch_post_passes(const int* ids, int n, const PostArgs& a, float* scratch, hipStream_t st);
+bool post_pass_needs_features(int id);
+bool post_pass_needs_shadow(int id);
 hipError_t launch_splat_shader(int id, const SplatShaderArgs& a, hipStream_t st);
 // texture names each shader samples (resolved by the host against the texture manager)
 const char* sh_shader_texture(int id, int k);

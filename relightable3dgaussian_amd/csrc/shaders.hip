@@ -278,6 +278,223 @@ bool splat_shader_needs_features(int id) {
            id == kSpRoughnessOnly || id == kSpQuantizeFlats || id == kSpQuantizeLight;
 }
 
+// ---- post-process passes (postProcessShader.cu:177-374, shaderUtils.cu) ----------------------
+bool post_pass_needs_features(int id) {
+    return id == kPpBlurLighting || id == kPpCrackReconstruction || id == kPpOutline || id == kPpQuantizeLighting ||
+           id == kPpTexturedShadows || id == kPpToon;
+}
+bool post_pass_needs_shadow(int id) { return id == kPpTexturedShadows || id == kPpToon; }
+
+// RgbToHsv / HsvToRgb (shaderUtils.cu:6-82)
+__device__ inline float3 rgb_to_hsv(float3 c) {
+    const float mx = fmaxf(c.x, fmaxf(c.y, c.z)), mn = fminf(c.x, fminf(c.y, c.z));
+    const float diff = mx - mn;
+    float h = 0.f, s = 0.f;
+    if (mx != 0.0f) {
+        s = diff / mx;
+        if (!(diff < 0.001f)) {
+            if (mx == c.x) {
+                h = (c.y - c.z) / diff / 6;
+                if (h < 0.0f) h += 1.0f;
+            } else if (mx == c.y) {
+                h = (2 + (c.z - c.x) / diff) / 6;
+            } else {
+                h = (4 + (c.x - c.y) / diff) / 6;
+            }
+        }
+    }
+    return make_float3(h, s, mx);
+}
+__device__ inline float3 hsv_to_rgb(float3 hsv) {
+    const float h = hsv.x, s = hsv.y, v = hsv.z;
+    float f = h * 6;
+    const float hi = floorf(f);
+    f = f - hi;
+    const float p = v * (1 - s), q = v * (1 - s * f), t = v * (1 - s * (1 - f));
+    if (hi == 0.0f || hi == 6.0f) return make_float3(v, t, p);
+    if (hi == 1.0f) return make_float3(q, v, p);
+    if (hi == 2.0f) return make_float3(p, v, t);
+    if (hi == 3.0f) return make_float3(p, q, v);
+    if (hi == 4.0f) return make_float3(t, p, v);
+    return make_float3(v, p, q);
+}
+
+// Sobel's unclamped depth reads (postProcessShader.cu:317-323): the reference's input buffer is
+// one allocation [21 feature planes | opacity | depth | stencil | xyz | ...]
+// (postProcessShader.cu:76-103), so reads above the first / below the last row land in the
+// opacity / stencil planes. None of those planes is written by a pass, so the live buffers hold
+// the same values as the reference's copy.
+__device__ inline float depth_in_buffer(const PostArgs& a, long long sp) {
+    const long long HW = (long long)a.W * a.H;
+    const long long k = 22 * HW + sp;
+    if (k >= 24 * HW) return k - 24 * HW < 3 * HW ? a.surface_xyz[k - 24 * HW] : 0.f;
+    if (k >= 23 * HW) return a.stencil[k - 23 * HW];
+    if (k >= 22 * HW) return a.depth[k - 22 * HW];
+    if (k >= 21 * HW) return a.opacity[k - 21 * HW];
+    return (a.features && k >= 0) ? a.features[k] : 0.f;
+}
+
+__device__ inline void pp_color_correction(const PostArgs& a, int p, float3 inc_in, float3& sc) {  // :276-289
+    const long long HW = (long long)a.W * a.H;
+    float3 hsv = rgb_to_hsv(f3(a.features + 9 * HW + 3 * (long long)p));
+    hsv.x = roundf(hsv.x * 24) / 24;  // Quantize(hue, 24)
+    const float3 color = hsv_to_rgb(hsv);
+    const float reduced = satf(inc_in.x + 0.25f);
+    sc = mul3(color, reduced);
+}
+
+__device__ inline void pp_textured_shadows(const PostArgs& a, int p, int x, int y, float3 inc_in, float3& sc) {  // :238-274
+    if (a.stencil[p] < 0.01f) {
+        sc = make_float3(1.f, 1.f, 1.f);
+        return;
+    }
+    const float uvScale = 10;
+    const float u = (float)x / (float)a.W * uvScale, v = (float)y / (float)a.H * uvScale;
+    const float4 t = tex_sample(a.shadow, u, v);
+    float lightShadow = 1 - t.x, mediumShadow = 1 - t.z, heavyShadow = 1 - t.y;
+    float intensity = inc_in.x > fmaxf(inc_in.y, inc_in.z) ? inc_in.x : fmaxf(inc_in.y, inc_in.z);  // __max
+    intensity = roundf(intensity * 4);
+    heavyShadow = satf(heavyShadow + intensity);
+    intensity = 0.f > intensity - 1.0f ? 0.f : intensity - 1.0f;
+    mediumShadow = satf(mediumShadow + intensity);
+    intensity = 0.f > intensity - 1.0f ? 0.f : intensity - 1.0f;
+    lightShadow = satf(lightShadow + intensity);
+    sc = mul3(mul3(mul3(sc, lightShadow), mediumShadow), heavyShadow);
+}
+
+__device__ inline void pp_sobel(const PostArgs& a, int p, float3& sc) {  // :304-331
+    const float SobelHorizontal[3][3] = {{-1, 0, 1}, {-2, 0, 2}, {-1, 0, 1}};
+    const float SobelVertical[3][3] = {{-1, -2, -1}, {0, 0, 0}, {1, 2, 1}};
+    const float outlineStrength = 2;
+    float hori = 0, vert = 0;
+    for (int x = -1; x < 2; x++)
+        for (int y = -1; y < 2; y++) {
+            const float d = depth_in_buffer(a, (long long)p + x + (long long)y * a.W);
+            hori += SobelHorizontal[x + 1][y + 1] * d * outlineStrength;
+            vert += SobelVertical[x + 1][y + 1] * d * outlineStrength;
+        }
+    const int depthChange = (int)sqrtf(powf(hori, 2.0f) + powf(vert, 2.0f));
+    sc = mul3(sc, satf((float)(1 - abs(depthChange))));
+}
+
+// One thread per pixel (the intended x + y * W mapping), every pass of a
+// pixel-local run in order. `in.*` reads of the pixel's own values are the live values at the
+// pass start: no other thread writes this pixel.
+__global__ void __launch_bounds__(256) post_pixel_kernel(PostArgs a) {
+    const long long HW = (long long)a.W * a.H;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= HW) return;
+    const int x = p % a.W, y = p / a.W;
+    float3 sc = f3(a.shader_color + 3 * (long long)p);
+    float* inc_ptr = a.features ? a.features + 12 * HW + 3 * (long long)p : nullptr;
+    float3 inc = inc_ptr ? f3(inc_ptr) : make_float3(0.f, 0.f, 0.f);
+    for (int i = 0; i < a.n_pass; ++i) {
+        const float3 sc_in = sc, inc_in = inc;
+        switch (a.pass[i]) {
+            case kPpInvert:  // :187-189
+                sc = sub3(make_float3(1.f, 1.f, 1.f), sc_in);
+                break;
+            case kPpOutline: {  // :212-232: the samples test in.pixel itself, so "near" == "inside"
+                const bool inside = a.stencil[p] >= 0.9f;
+                const bool near = inside;
+                const float o = (float)(!inside && near);
+                const float3 base = f3(a.features + 9 * HW + 3 * (long long)p);
+                sc = add3(mul3(base, 1.0f - o), mul3(make_float3(1.f, 0.f, 0.f), o));
+                break;
+            }
+            case kPpCrackReconstruction: {  // :234-261
+                const float mask = a.stencil[p] * a.features[HW + p];
+                if (mask <= 0.01f) break;
+                const float3 normal = f3(a.pseudonormal + 3 * (long long)p);
+                const float3 lightDir = norm3(make_float3(0.f, -0.2f, 1.f));
+                const float lightIntensity = 0.1f, ambientLight = 0.9f;
+                float3 internal = make_float3(0.83f, 0.64f, 0.2f);
+                internal = mul3(internal, satf(satf(dot3(lightDir, normal) * lightIntensity) + ambientLight));
+                sc = add3(mul3(internal, mask), mul3(sc_in, 1 - mask));
+                break;
+            }
+            case kPpTexturedShadows:
+                pp_textured_shadows(a, p, x, y, inc_in, sc);
+                break;
+            case kPpQuantizeLighting: {  // :291-297
+                const float white = fmaxf(inc_in.x, fmaxf(inc_in.y, inc_in.z));
+                const float q = roundf(white * 4) / 4;
+                inc = make_float3(q, q, q);
+                break;
+            }
+            case kPpSobelFilter:
+                pp_sobel(a, p, sc);
+                break;
+            case kPpToon:  // :333-337
+                pp_color_correction(a, p, inc_in, sc);
+                pp_textured_shadows(a, p, x, y, inc_in, sc);
+                pp_sobel(a, p, sc);
+                break;
+            default:
+                break;
+        }
+    }
+    st3(a.shader_color + 3 * (long long)p, sc);
+    if (inc_ptr) st3(inc_ptr, inc);
+}
+
+// BlurLighting (:299-309) with GaussianBlur's clamped 1-D neighbourhood (shaderUtils.cu:104-123)
+__constant__ float kBlend[5][5] = {{0.009375f, 0.01875f, 0.028125f, 0.01875f, 0.009375f},
+                                   {0.01875f, 0.0375f, 0.045f, 0.0375f, 0.01875f},
+                                   {0.028125f, 0.045f, 0.3f, 0.045f, 0.028125f},
+                                   {0.01875f, 0.0375f, 0.045f, 0.0375f, 0.01875f},
+                                   {0.009375f, 0.01875f, 0.028125f, 0.01875f, 0.009375f}};
+__global__ void __launch_bounds__(256) post_blur_kernel(PostArgs a) {
+    const int HW = a.W * a.H;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= HW) return;
+    const float3 pix = f3(a.incident_in + 3 * (size_t)p);
+    if (pix.x == 0 && pix.y == 0 && pix.z == 0) return;
+    float3 acc = make_float3(0.f, 0.f, 0.f);
+    for (int x = -2; x < 3; x++)
+        for (int y = -2; y < 3; y++) {
+            int sp = p + x + y * a.W;
+            sp = max(0, min(HW - 1, sp));
+            acc = add3(acc, mul3(f3(a.incident_in + 3 * (size_t)sp), kBlend[x + 2][y + 2]));
+        }
+    st3(a.features + 12 * (size_t)HW + 3 * (size_t)p, acc);
+}
+
+hipError_t launch_post_passes(const int* ids, int n, const PostArgs& base, float* scratch, hipStream_t st) {
+    const int HW = base.W * base.H;
+    if (HW == 0) return hipSuccess;
+    const dim3 grid((HW + 255) / 256), block(256);
+    PostArgs a = base;
+    a.n_pass = 0;
+    auto flush = [&]() -> hipError_t {
+        if (a.n_pass == 0) return hipSuccess;
+        hipLaunchKernelGGL(post_pixel_kernel, grid, block, 0, st, a);
+        a.n_pass = 0;
+        return hipGetLastError();
+    };
+    for (int i = 0; i < n; ++i) {
+        const int id = ids[i];
+        if (id == kPpDefault) continue;  // DefaultPostProcess does nothing
+        if (id == kPpBlurLighting) {
+            hipError_t e = flush();
+            if (e != hipSuccess) return e;
+            e = hipMemcpyAsync(scratch, a.features + 12 * (size_t)HW, sizeof(float) * 3 * (size_t)HW,
+                               hipMemcpyDeviceToDevice, st);
+            if (e != hipSuccess) return e;
+            a.incident_in = scratch;
+            hipLaunchKernelGGL(post_blur_kernel, grid, block, 0, st, a);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            continue;
+        }
+        if (a.n_pass == kMaxFusedPasses) {
+            const hipError_t e = flush();
+            if (e != hipSuccess) return e;
+        }
+        a.pass[a.n_pass++] = id;
+    }
+    return flush();
+}
+
 // ---- texture objects (texture.cu:86-262) ----------------------------------------------------
 // Texel expansion: 1-channel modes go to .x (alpha 1), 3-channel modes get alpha 1
 // (CreatPaddedArrayFromBase), 4-channel modes are copied.

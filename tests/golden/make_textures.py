@@ -12,7 +12,7 @@ from PIL import Image
 
 SRC = "/root/reference/textures"
 FILES = {"Cracks": "Cracks 2.png", "Turbulence": "Turbulence 2.png", "Craters": "Craters 12.png",
-         "Depth cracks": "Depth Cracks.png", "Bulge": "bulge.png", "Error": "Error.png"}
+         "Depth cracks": "Depth Cracks.png", "Bulge": "bulge.png", "shadow": "shadow.png", "Error": "Error.png"}
 
 out = {}
 for name, f in FILES.items():
