@@ -255,10 +255,11 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     constexpr int NXB = (4 + SMAX + 15) / 16;     // 16-channel blocks of X = [g0..2, gf0..S-1, gd]
     constexpr int WQS = 66;                       // padded LDS row stride of the w|q image
     constexpr int GRP = 8;                        // instances per MFMA group: rows 0..7 w, 8..15 q
+    constexpr int RF4 = 2 + NA4;                  // float4s per render record in HBM
+    constexpr int SF4 = 1 + NA4;                  // staged: conic|opacity, attribute row
+    __shared__ float4 s_rec[kBlock * SF4];        // one base address per instance
     __shared__ float2 s_xy[kBlock];
-    __shared__ float4 s_co[kBlock];
     __shared__ uint32_t s_slot[kBlock];
-    __shared__ float4 s_attr[kBlock * NA4];
     __shared__ uint32_t s_bits[8][4];             // [chunk][wave] live-instance masks
     __shared__ float4 s_part4[4 * CH * RSL / 4];  // [wave][chunk instance][RSL]
     __shared__ float s_wq[4][16 * WQS];           // per wave: rows 0..7 w, 8..15 q; [row][pixel]
@@ -327,14 +328,19 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
         yC = nch == 5 ? 1.f : 0.f;
     }
 
-    // The reference keeps one accum_rec per channel (colour, features, depth); all share the same
-    // alpha recurrence and enter dL/dalpha only through their dot with the upstream gradient, so one
-    // scalar acc_dot = sum_c accum_rec[c] * dL_dchannel[c] carries them all.
+    // The reference keeps one accum_rec per channel (colour, features, depth) and accum_opa; all
+    // share the same alpha recurrence and enter dL/dalpha only through their dot with the upstream
+    // gradient, so one scalar u = sum_c accum_rec[c] * dL_dchannel[c] + dL_dopacity * accum_opa
+    // carries them all. With d = colour.g + dL_dopacity: dL/dalpha = (d - u) * T' - T_final /
+    // (1 - alpha) * bg.g, then u += alpha * (d - u) -- the reference's delayed last_alpha /
+    // last_color update applied at the end of each contributing step instead. A non-contributing
+    // step runs with alpha = 0, which leaves T (1/(1-0) = 1 exactly) and u unchanged.
     if (!a.backward_geometry) {
 #pragma unroll
         for (int c = 0; c < SMAX; ++c) gf[c] = 0.f;  // bX already holds the feature grads
     }
-    float acc_dot = 0.f, last_dot = 0.f, acc_o = 0.f, last_alpha = 0.f;
+    float u = 0.f;
+    const float TFB = T_final * bg_dot;
 
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
     if (t == 0) s_max_last = 0;
@@ -370,16 +376,17 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
         if (t < cnt) {
             const uint32_t k = range.x + (uint32_t)(hi - 1 - t);
             const uint32_t gid = a.point_list[k];
-            // one contiguous render record per Gaussian (r3dg_kernels.h record_f4)
-            const float4* rec = a.records + (size_t)gid * (2 + NA4);
-            const float4 co = rec[0], r1 = rec[1];
-            const float2 xy = make_float2(r1.x, r1.y);
-            s_slot[t] = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
-            s_xy[t] = xy;
-            s_co[t] = co;
-            m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
+            // one contiguous render record per Gaussian (r3dg_kernels.h record_f4), staged verbatim
+            const float4* rec = a.records + (size_t)gid * RF4;
+            float4 r[RF4];
 #pragma unroll
-            for (int q = 0; q < NA4; ++q) s_attr[t * NA4 + q] = rec[2 + q];
+            for (int q = 0; q < RF4; ++q) r[q] = rec[q];
+            s_rec[t * SF4] = r[0];
+#pragma unroll
+            for (int q = 0; q < NA4; ++q) s_rec[t * SF4 + 1 + q] = r[2 + q];
+            s_xy[t] = make_float2(r[1].x, r[1].y);
+            s_slot[t] = record_slot(r[1], tx, ty, a.grid_x, a.grid_y);
+            m = quadrant_mask(make_float2(r[1].x, r[1].y), r[0], tx * kTileX, ty * kTileY, a.cull);
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -402,38 +409,38 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             // (outside, past n_contrib, power > 0 or alpha < 1/255) leaves its state unchanged.
             auto step = [&](int j, bool live, float& wv, float& qv) {
 #pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
-                const float2 xy = s_xy[j];
-                const float4 co = s_co[j];
+                const int ju = __builtin_amdgcn_readfirstlane(j);  // uniform addresses
+                const float4* rj = s_rec + ju * SF4;
+                const float4 co = rj[0];
+                const float2 xy = s_xy[ju];
                 float v[NA4 * 4];
 #pragma unroll
                 for (int q = 0; q < NA4; ++q) {
-                    const float4 rr = s_attr[j * NA4 + q];
+                    const float4 rr = rj[1 + q];
                     v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
                 }
                 const int p = hi - 1 - j;  // position in the tile range (reference `contributor`)
                 const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
                 const float G = __expf(power);
                 const float alpha = fminf(0.99f, co.w * G);
-                const bool ok = live && inside && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-                const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
+                // p < last is false for pixels outside the image (last = 0 there)
+                const bool ok = live && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const float ae = ok ? alpha : 0.f;
+                const float Ge = ok ? G : 0.f;
+                const float rinv = __builtin_amdgcn_rcpf(1.f - ae);
                 const float Tn = T * rinv;
-                float dot = v[0] * g[0];
-                dot = __builtin_fmaf(v[1], g[1], dot);
-                dot = __builtin_fmaf(v[2], g[2], dot);
-                dot = __builtin_fmaf(v[3], gd, dot);
+                float d = __builtin_fmaf(v[0], g[0], go);
+                d = __builtin_fmaf(v[1], g[1], d);
+                d = __builtin_fmaf(v[2], g[2], d);
+                d = __builtin_fmaf(v[3], gd, d);
 #pragma unroll
-                for (int c2 = 0; c2 < SMAX; ++c2) dot = __builtin_fmaf(v[4 + c2], gf[c2], dot);
-                const float acc_dot_n = __builtin_fmaf(last_alpha, last_dot, (1.f - last_alpha) * acc_dot);
-                const float acc_o_n = __builtin_fmaf(1.f - last_alpha, acc_o, last_alpha);
-                float dL_dalpha = __builtin_fmaf(1.0f - acc_o_n, go, dot - acc_dot_n);
-                dL_dalpha = __builtin_fmaf(dL_dalpha, Tn, (-T_final * rinv) * bg_dot);
-                wv = ok ? alpha * Tn : 0.f;
-                qv = ok ? G * dL_dalpha : 0.f;
-                T = ok ? Tn : T;
-                acc_dot = ok ? acc_dot_n : acc_dot;
-                last_dot = ok ? dot : last_dot;
-                acc_o = ok ? acc_o_n : acc_o;
-                last_alpha = ok ? alpha : last_alpha;
+                for (int c2 = 0; c2 < SMAX; ++c2) d = __builtin_fmaf(v[4 + c2], gf[c2], d);
+                const float diff = d - u;
+                const float dL_dalpha = rinv * __builtin_fmaf(T, diff, -TFB);
+                wv = ae * Tn;
+                qv = Ge * dL_dalpha;
+                T = Tn;
+                u = __builtin_fmaf(ae, diff, u);
             };
             while (bits) {
                 // two compacted instances per iteration: the second one's LDS reads and exp
@@ -513,7 +520,7 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
                         src[1] = make_float4(0.f, 0.f, 0.f, 0.f);
                     }
                     const float2 xy = s_xy[j];
-                    const float4 co = s_co[j];
+                    const float4 co = s_rec[j * SF4];
                     // slots: 0 Sx, 1 Sy, 2 depth, 3 Sxx, 4 Sxy, 5 Syy, 6 S0 (= opacity grad), 7 colour r
                     const float S0 = u1.z, Sx = u0.x, Sy = u0.y, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
                     const float d0x = xy.x - ctx, d0y = xy.y - cty;
