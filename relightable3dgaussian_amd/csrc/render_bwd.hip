@@ -245,22 +245,38 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// Tuning knobs (experiment builds override them through R3DG_EXTRA_HIPFLAGS). Occupancy is
+// set by LDS and VGPRs together; the LDS allocation is rounded up in 2 KiB steps (54,020 B ran
+// at two workgroups per CU: 1.63 -> 2.09 ms). The defaults -- 128-instance staging batches and
+// a 65-float w|q row stride -- give 40,900 B (four workgroups per CU) and 127 VGPRs (four
+// waves per SIMD): 1.63 -> 1.45 ms at M1 against 256 / 66 / three waves.
+#ifndef R3DG_BWD_NB
+#define R3DG_BWD_NB 128  // instances staged per batch
+#endif
+#ifndef R3DG_BWD_WQS
+#define R3DG_BWD_WQS 65  // padded LDS row stride of the w|q image
+#endif
+#ifndef R3DG_BWD_WAVES
+#define R3DG_BWD_WAVES 4  // waves per SIMD the register allocation targets (SMAX <= 12)
+#endif
+
 template <int SMAX>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? 3 : 1)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
 render_bwd_mfma_kernel(RenderBwdArgs a) {
+    constexpr int NB = R3DG_BWD_NB;
     constexpr int NA4 = (4 + SMAX + 3) / 4;       // staged attribute row: colour, depth, features
     constexpr int NR = kRowFeat + SMAX;
     constexpr int RSL = (NR + 3) & ~3;            // LDS partial row stride (floats)
     constexpr int CH = 32;                        // instances per flush chunk (= one compaction mask)
     constexpr int NXB = (4 + SMAX + 15) / 16;     // 16-channel blocks of X = [g0..2, gf0..S-1, gd]
-    constexpr int WQS = 66;                       // padded LDS row stride of the w|q image
+    constexpr int WQS = R3DG_BWD_WQS;             // padded LDS row stride of the w|q image
     constexpr int GRP = 8;                        // instances per MFMA group: rows 0..7 w, 8..15 q
     constexpr int RF4 = 2 + NA4;                  // float4s per render record in HBM
     constexpr int SF4 = 1 + NA4;                  // staged: conic|opacity, attribute row
-    __shared__ float4 s_rec[kBlock * SF4];        // one base address per instance
-    __shared__ float2 s_xy[kBlock];
-    __shared__ uint32_t s_slot[kBlock];
-    __shared__ uint32_t s_bits[8][4];             // [chunk][wave] live-instance masks
+    __shared__ float4 s_rec[NB * SF4];            // one base address per instance
+    __shared__ float2 s_xy[NB];
+    __shared__ uint32_t s_slot[NB];
+    __shared__ uint32_t s_bits[NB / 32][4];       // [chunk][wave] live-instance masks
     __shared__ float4 s_part4[4 * CH * RSL / 4];  // [wave][chunk instance][RSL]
     __shared__ float s_wq[4][16 * WQS];           // per wave: rows 0..7 w, 8..15 q; [row][pixel]
     __shared__ int s_rowid[4][GRP];
@@ -369,8 +385,8 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     const float ctx = (float)(tx * kTileX) + 7.5f, cty = (float)(ty * kTileY) + 7.5f;
     const bool x_half = (l >> 4) < 2;  // result rows 0..7 (w . X) live in lanes 0..31, 8..15 (q . Y) in 32..63
 
-    for (int hi = max_last; hi > 0; hi -= kBlock) {
-        const int cnt = min(kBlock, hi);
+    for (int hi = max_last; hi > 0; hi -= NB) {
+        const int cnt = min(NB, hi);
         __syncthreads();
         uint32_t m = 0;
         if (t < cnt) {
@@ -391,7 +407,7 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const unsigned long long bal = __ballot((m >> b) & 1u);
-            if (l == 0) {
+            if (l == 0 && w < NB / 64) {
                 s_bits[2 * w][b] = (uint32_t)bal;
                 s_bits[2 * w + 1][b] = (uint32_t)(bal >> 32);
             }
