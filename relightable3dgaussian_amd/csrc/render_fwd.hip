@@ -20,15 +20,27 @@
 
 namespace r3dg {
 
+// Tuning knobs (experiment builds override them through R3DG_EXTRA_HIPFLAGS).
+#ifndef R3DG_FWD_NB
+#define R3DG_FWD_NB 256  // instances staged per batch
+#endif
+#ifndef R3DG_FWD_WAVES
+#define R3DG_FWD_WAVES 6  // waves per SIMD the register allocation targets (SMAX <= 12)
+#endif
+#ifndef R3DG_FWD_PAIR
+#define R3DG_FWD_PAIR 1  // two compacted instances per loop iteration
+#endif
+
 template <int SMAX, bool SHADER>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? 6 : 1)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_FWD_WAVES : 1)))
 render_fwd_kernel(RenderFwdArgs a) {
+    constexpr int NB = R3DG_FWD_NB;
     constexpr int FO = SHADER ? 8 : 4;                 // feature offset inside the attribute row
     constexpr int NA4 = (FO + SMAX + 3) / 4;           // float4 per attribute row
-    __shared__ float2 s_xy[kBlock];
-    __shared__ float4 s_co[kBlock];
-    __shared__ float4 s_attr[kBlock * NA4];
-    __shared__ uint32_t s_bits[8][4];                  // [32-instance chunk][wave]: live-instance masks
+    __shared__ float2 s_xy[NB];
+    __shared__ float4 s_co[NB];
+    __shared__ float4 s_attr[NB * NA4];
+    __shared__ uint32_t s_bits[NB / 32][4];            // [32-instance chunk][wave]: live-instance masks
 
     const int tile = block_tile(a.tile_order, a.num_tiles);
     if (tile >= a.num_tiles) return;
@@ -49,10 +61,10 @@ render_fwd_kernel(RenderFwdArgs a) {
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) F[c] = 0.f;
 
-    for (int base = 0; base < n; base += kBlock) {
+    for (int base = 0; base < n; base += NB) {
         if (__syncthreads_count(done) == kBlock) break;
         uint32_t m = 0;
-        if (base + t < n) {
+        if (t < NB && base + t < n) {
             const uint32_t gid = a.point_list[range.x + base + t];
             if constexpr (!SHADER) {
                 // one contiguous render record per Gaussian (r3dg_kernels.h record_f4)
@@ -95,7 +107,7 @@ render_fwd_kernel(RenderFwdArgs a) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const unsigned long long bal = __ballot((m >> b) & 1u);
-            if (l == 0) {
+            if (l == 0 && w < NB / 64) {
                 s_bits[2 * w][b] = (uint32_t)bal;
                 s_bits[2 * w + 1][b] = (uint32_t)(bal >> 32);
             }
@@ -138,9 +150,10 @@ render_fwd_kernel(RenderFwdArgs a) {
             }
         };
         bool alive = __ballot(!done) != 0ull;
-        for (int c = 0; c < 8 && alive; ++c) {
+        for (int c = 0; c < NB / 32 && alive; ++c) {
             uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[c][w]);
             while (bits) {
+#if R3DG_FWD_PAIR
                 // two compacted instances per iteration (the second one's reads overlap the first)
                 const int j0 = c * 32 + __builtin_ctz(bits);
                 bits &= bits - 1;
@@ -149,6 +162,11 @@ render_fwd_kernel(RenderFwdArgs a) {
                 bits &= bits - 1;
                 step(j0, true);
                 step(j1, has1);
+#else
+                const int j0 = c * 32 + __builtin_ctz(bits);
+                bits &= bits - 1;
+                step(j0, true);
+#endif
                 if (__ballot(!done) == 0ull) {  // converged here: a uniform exit
                     alive = false;
                     break;
