@@ -28,7 +28,7 @@ def _load_ext():
     if not os.path.exists(EXT_LIB) or not os.path.exists(HIP_LIB):
         raise ImportError(
             "relightable3dgaussian_amd: native extension not built (expected %s and %s); run "
-            "`python -m relightable3dgaussian_amd.build` or __graft_entry__.build()" % (HIP_LIB, EXT_LIB))
+            "`python relightable3dgaussian_amd/build.py` or __graft_entry__.build()" % (HIP_LIB, EXT_LIB))
     loader = importlib.machinery.ExtensionFileLoader("relightable3dgaussian_amd._C", EXT_LIB)
     spec = importlib.util.spec_from_file_location("relightable3dgaussian_amd._C", EXT_LIB, loader=loader)
     mod = importlib.util.module_from_spec(spec)

@@ -4,7 +4,7 @@ Produces (git-ignored, but shipped to the GPU box with the tree):
   relightable3dgaussian_amd/lib/libr3dg_hip.so   -- HIP kernels + the C ABI of include/r3dg_hip.h
   relightable3dgaussian_amd/lib/_C.so             -- pybind module mirroring r3dg_rasterization._C
 
-`python -m relightable3dgaussian_amd.build` rebuilds what is out of date. hipcc cross-compiles
+`python relightable3dgaussian_amd/build.py` rebuilds what is out of date. hipcc cross-compiles
 for gfx950 without a GPU, so this runs in the CPU container too.
 """
 from __future__ import annotations
