@@ -19,7 +19,7 @@ import sys
 import torch  # noqa: F401  (loads libtorch / the HIP runtime before our libraries)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_DIR = os.path.join(_PKG, "lib")
+LIB_DIR = os.environ.get("R3DG_LIB_DIR") or os.path.join(_PKG, "lib")  # override: experiment builds
 HIP_LIB = os.path.join(LIB_DIR, "libr3dg_hip.so")
 EXT_LIB = os.path.join(LIB_DIR, "_C.so")
 

@@ -18,9 +18,10 @@ from concurrent.futures import ThreadPoolExecutor
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-LIB = os.path.join(PKG, "lib")
+# experiment builds put their objects / libraries elsewhere (tools/exp_build.sh)
+LIB = os.environ.get("R3DG_LIB_DIR") or os.path.join(PKG, "lib")
 INC = os.path.join(ROOT, "include")
-OBJ = os.path.join(PKG, "build", "obj")
+OBJ = os.environ.get("R3DG_OBJ_DIR") or os.path.join(PKG, "build", "obj")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 

@@ -57,10 +57,19 @@ struct RenderFwdArgs {
     FeatureLayout flay;
 };
 
-// Per-instance gradient row written by the backward blend: [mean2D x,y,z | conic x,y,w |
-// opacity | colour r,g,b | features 0..S-1 | pad], RS floats (multiple of 4).
+// Per-Gaussian gradient sums the gather kernel assembles (LDS, one row per Gaussian):
+// [mean2D x,y,z | conic x,y,w | opacity | colour r,g,b | features 0..S-1 | pad].
 constexpr int kRowMean = 0, kRowConic = 3, kRowOpacity = 6, kRowColor = 7, kRowFeat = 10;
-__host__ __device__ inline int row_stride(int S) { return ((kRowFeat + S) + 3) & ~3; }
+
+// Partial gradient row written by the backward blend for one (instance, 8x8 quadrant) pair --
+// the reduction of one wave's 64 pixels, at index 4 * slot + quadrant:
+//   [0, XW)      X part: sum_px w * [dL/dcolour 0..2, dL/dfeature 0..S-1, dL/ddepth], zero pad
+//   [XW, XW+6)   moments of q = G * dL/dalpha about the quadrant centre (pixel offsets x, y in
+//                -3.5 .. 3.5): sum q * [1, x, y, x^2, xy, y^2]; then 2 pad floats
+// with w = alpha * T and XW = 16 * bwd_xblocks(S). A row exists only where the wave blended the
+// instance; flags[4 * slot + quadrant] = 1 marks it (the gather reads flagged rows only).
+__host__ __device__ inline int bwd_xblocks(int S);
+__host__ __device__ inline int part_row_stride(int S);
 
 struct RenderBwdArgs {
     const float4* records;     // render records (record_f4)
@@ -84,12 +93,18 @@ struct RenderBwdArgs {
     FeatureLayout gflay;
     int S, W, H, grid_x, grid_y, num_tiles, cull, backward_geometry, RS;
     const uint32_t* tile_order;  // launch order of the tiles (longest first), or null
-    float* rows;               // [L, RS]
+    float* rows;               // [4L, RS] partial rows (part_row_stride)
+    uint8_t* flags;            // [4L] 1 where a partial row was written (zeroed by the host)
 };
 
 struct GatherBwdArgs {
-    int P, D, M, S, RS;
-    const float* rows;
+    int P, D, M, S, RS, W, H, grid_x, grid_y;
+    const float* rows;        // partial rows (RenderBwdArgs)
+    const float* zero_row;    // RS zeros: the load target of quadrants without a row
+    float* sums;              // [P, RS] per-Gaussian sums (row_sum_kernel -> gather_bwd_kernel)
+    const uint32_t* flags;    // one word per slot: byte q set when quadrant q's row exists
+    const float2* means2D;
+    const float4* conic_opacity;
     const uint32_t* offsets;
     const int* radii;
     const float* means3D;
@@ -183,6 +198,8 @@ __host__ __device__ inline int smax_of(int S) {
     return S == 0 ? 0 : S <= 4 ? 4 : S <= 8 ? 8 : S <= 12 ? 12 : S <= 16 ? 16 : S <= 24 ? 24 : 32;
 }
 __host__ __device__ inline int record_f4(int S) { return 2 + (4 + smax_of(S) + 3) / 4; }
+__host__ __device__ inline int bwd_xblocks(int S) { return (4 + smax_of(S) + 15) / 16; }
+__host__ __device__ inline int part_row_stride(int S) { return 16 * bwd_xblocks(S) + 8; }
 
 __host__ __device__ inline int padded_tile_grid(int num_tiles) { return (num_tiles + 7) & ~7; }
 __device__ __forceinline__ int xcd_tile(int b, int grid) {
@@ -198,5 +215,15 @@ __device__ __forceinline__ int block_tile(const uint32_t* order, int num_tiles) 
     return xcd_tile(b, gridDim.x);
 }
 __global__ void tile_count_kernel(int T, const uint2* ranges, uint32_t* counts);
+#ifdef R3DG_EXP_COUNT  // timing/counting experiment builds only (tools/exp_build.sh)
+static __device__ unsigned long long g_exp_cnt[8];  // one copy per translation unit
+#define R3DG_EXP_READER(name)                                                        \
+    extern "C" void name(unsigned long long* out) {                                  \
+        hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_cnt), sizeof(g_exp_cnt));         \
+    }
+#define R3DG_EXP_ADD(i, v) atomicAdd(&g_exp_cnt[i], (unsigned long long)(v))
+#else
+#define R3DG_EXP_ADD(i, v) ((void)0)
+#endif
 
 }  // namespace r3dg

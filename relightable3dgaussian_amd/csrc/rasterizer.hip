@@ -734,14 +734,24 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     BinningState bs = binning_state_from(binning, (size_t)L);
     ImageState is = image_state_from(image, H, W);
     const int* radii = radii_in ? radii_in : gs.internal_radii;
-    const int RS = row_stride(S);
-    float* rows = nullptr;
+    const int RS = part_row_stride(S);
+    // scratch: partial rows [4L, RS] (one per instance and quadrant, written sparsely), per-Gaussian
+    // sums [P, RS], one zero row (the gather's load target for absent rows), flags [4L]; the zero
+    // row and the flags are cleared by one memset
+    const size_t row_bytes = sizeof(float) * (size_t)RS * 4 * L;
+    const size_t sum_bytes = sizeof(float) * (size_t)RS * P;
+    const size_t zero_bytes = sizeof(float) * (size_t)RS;
+    char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + sum_bytes + zero_bytes + 4 * (size_t)L);
+    if (!scratch) {
+        set_error("rasterize_gaussians_backward: scratch allocation failed");
+        return R3DG_ERR_ALLOC;
+    }
+    float* rows = L > 0 ? reinterpret_cast<float*>(scratch) : nullptr;
+    float* sums = reinterpret_cast<float*>(scratch + row_bytes);
+    float* zero_row = reinterpret_cast<float*>(scratch + row_bytes + sum_bytes);
+    uint8_t* flags = reinterpret_cast<uint8_t*>(scratch + row_bytes + sum_bytes + zero_bytes);
+    R3DG_CHECK_HIP(hipMemsetAsync(zero_row, 0, zero_bytes + 4 * (size_t)L, st));
     if (L > 0) {
-        rows = (float*)scratch_alloc(scratch_ctx, sizeof(float) * (size_t)RS * L);
-        if (!rows) {
-            set_error("rasterize_gaussians_backward: scratch allocation failed");
-            return R3DG_ERR_ALLOC;
-        }
         RenderBwdArgs ba{};
         ba.records = gs.records;
         ba.ranges = is.ranges;
@@ -772,6 +782,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         ba.backward_geometry = backward_geometry;
         ba.RS = RS;
         ba.rows = rows;
+        ba.flags = flags;
         {
             ProfScope ps(R3DG_PROF_RENDER_BWD, st);
             R3DG_CHECK_HIP(launch_render_backward(ba, st));
@@ -780,7 +791,13 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     }
     GatherBwdArgs ga{};
     ga.P = P; ga.D = s->D; ga.M = s->M; ga.S = S; ga.RS = RS;
+    ga.W = W; ga.H = H; ga.grid_x = gx; ga.grid_y = gy;
     ga.rows = rows;
+    ga.zero_row = zero_row;
+    ga.sums = sums;
+    ga.flags = reinterpret_cast<const uint32_t*>(flags);
+    ga.means2D = gs.means2D;
+    ga.conic_opacity = gs.conic_opacity;
     ga.offsets = gs.point_offsets;
     ga.radii = radii;
     ga.means3D = g->means3D;

@@ -20,54 +20,71 @@
 
 namespace r3dg {
 
+#ifdef R3DG_EXP_COUNT
+R3DG_EXP_READER(r3dg_exp_counters_bwd)
+#endif
+
 __device__ __forceinline__ int wave_max_int(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
     return v;
 }
 
+// Pixel setup shared by both variants: lane l of wave w owns pixel (l & 7, l >> 3) of the tile's
+// 8x8 quadrant w; the upstream gradients of that pixel.
+#define R3DG_BWD_PIXEL_SETUP()                                                                          \
+    const int tile = block_tile(a.tile_order, a.num_tiles);                                             \
+    if (tile >= a.num_tiles) return;                                                                    \
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;                                               \
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;                                                  \
+    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);                                                 \
+    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);                                               \
+    const bool inside = px < a.W && py < a.H;                                                           \
+    const int pix = inside ? py * a.W + px : 0;                                                         \
+    const float pfx = (float)px, pfy = (float)py;                                                       \
+    const uint2 range = a.ranges[tile];                                                                 \
+    const int S = a.S;                                                                                  \
+    const float T_final = inside ? a.final_T[pix] : 0.f;                                                \
+    const int last = inside ? (int)a.n_contrib[pix] : 0;                                                \
+    float g[3], gf[SMAX > 0 ? SMAX : 1], gd = 0.f, go = 0.f;                                            \
+    _Pragma("unroll") for (int c = 0; c < 3; ++c) g[c] = inside ? a.dL_dpix[a.ca[c] + pix * a.cm[c]] : 0.f; \
+    _Pragma("unroll") for (int c = 0; c < SMAX; ++c) gf[c] =                                            \
+        (inside && c < S) ? a.dL_dpix_f[a.gflay.a[c] + pix * a.gflay.m[c]] : 0.f;                       \
+    if (inside) {                                                                                       \
+        gd = a.dL_dpix_d[pix];                                                                          \
+        go = a.dL_dpix_o[pix];                                                                          \
+    }                                                                                                   \
+    const float bg_dot = a.bg[0] * g[0] + a.bg[1] * g[1] + a.bg[2] * g[2];
+
+// Block-wide max of n_contrib: tile positions >= it are never blended (and never staged).
+__device__ __forceinline__ int block_max_last(int wmax, int* s_max_last) {
+    if (threadIdx.x == 0) *s_max_last = 0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) atomicMax(s_max_last, wmax);
+    __syncthreads();
+    return *s_max_last;
+}
+
+// DPP variant (cross-check of the MFMA default, R3DG_BWD=dpp): the reference's per-channel
+// recurrences (backward.cu:544-579) step by step; every wave reduces its 64 pixels' values of an
+// instance with DPP and lane 63 writes the wave's partial row.
 template <int SMAX>
 __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a) {
     constexpr int NA4 = (4 + SMAX + 3) / 4;      // attribute row: colour, depth, features
-    constexpr int NR = kRowFeat + SMAX;          // reduced values per instance
-    constexpr int RSL = (NR + 3) & ~3;           // LDS partial row stride (floats)
-    constexpr int CH = 64;                       // instances per flush chunk
+    constexpr int NXB = (4 + SMAX + 15) / 16;
+    constexpr int XW = 16 * NXB;
+    constexpr int RF4 = 2 + NA4;
     __shared__ float2 s_xy[kBlock];
     __shared__ float4 s_co[kBlock];
     __shared__ uint32_t s_mask[kBlock];
     __shared__ uint32_t s_slot[kBlock];
     __shared__ float4 s_attr[kBlock * NA4];
-    __shared__ float4 s_part4[4 * CH * RSL / 4];  // [wave][chunk instance][RSL]
     __shared__ int s_max_last;
-    float* s_part = reinterpret_cast<float*>(s_part4);
 
-    const int tile = block_tile(a.tile_order, a.num_tiles);
-    if (tile >= a.num_tiles) return;
-    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
-    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
-    const bool inside = px < a.W && py < a.H;
-    const int pix = inside ? py * a.W + px : 0;
-    const float pfx = (float)px, pfy = (float)py;
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
-
-    const float T_final = inside ? a.final_T[pix] : 0.f;
+    R3DG_BWD_PIXEL_SETUP()
     float T = T_final;
-    const int last = inside ? (int)a.n_contrib[pix] : 0;
-    float g[3], gf[SMAX > 0 ? SMAX : 1], gd = 0.f, go = 0.f;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) g[c] = inside ? a.dL_dpix[a.ca[c] + pix * a.cm[c]] : 0.f;
-#pragma unroll
-    for (int c = 0; c < SMAX; ++c)
-        gf[c] = (inside && c < a.S) ? a.dL_dpix_f[a.gflay.a[c] + pix * a.gflay.m[c]] : 0.f;
-    if (inside) {
-        gd = a.dL_dpix_d[pix];
-        go = a.dL_dpix_o[pix];
-    }
-    const float bg_dot = a.bg[0] * g[0] + a.bg[1] * g[1] + a.bg[2] * g[2];
     const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
+    const float xr = (float)(l & 7) - 3.5f, yr = (float)(l >> 3) - 3.5f;  // offset from the quadrant centre
 
     float acc[3] = {0.f, 0.f, 0.f}, acc_f[SMAX > 0 ? SMAX : 1], acc_d = 0.f, acc_o = 0.f;
     float last_alpha = 0.f, last_depth = 0.f, last_color[3] = {0.f, 0.f, 0.f}, last_f[SMAX > 0 ? SMAX : 1];
@@ -76,166 +93,119 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
         acc_f[c] = 0.f;
         last_f[c] = 0.f;
     }
-
-    // Positions >= max(n_contrib) over the tile are never blended: their rows are zero.
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
-    if (t == 0) s_max_last = 0;
-    for (int i = t; i < 4 * CH * RSL / 4; i += kBlock) s_part4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    __syncthreads();
-    if (l == 0) atomicMax(&s_max_last, wmax);
-    __syncthreads();
-    const int max_last = s_max_last;
+    const int max_last = block_max_last(wmax, &s_max_last);
     const int RS = a.RS;
-    for (int p = max_last + t; p < n; p += kBlock) {
-        const uint32_t gid = a.point_list[range.x + p];
-        const uint32_t slot = instance_slot(a.offsets, a.means2D[gid], a.radii[gid], gid, tx, ty, a.grid_x, a.grid_y);
-        float4* row = reinterpret_cast<float4*>(a.rows + (size_t)slot * RS);
-        for (int q = 0; q < RS / 4; ++q) row[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    (void)ddelx_dx;
+    (void)ddely_dy;
 
     for (int hi = max_last; hi > 0; hi -= kBlock) {
         const int cnt = min(kBlock, hi);
         __syncthreads();  // previous batch fully consumed before the staging arrays are reused
         if (t < cnt) {
-            const uint32_t k = range.x + (uint32_t)(hi - 1 - t);
-            const uint32_t gid = a.point_list[k];
-            const float2 xy = a.means2D[gid];
-            s_slot[t] = instance_slot(a.offsets, xy, a.radii[gid], gid, tx, ty, a.grid_x, a.grid_y);
-            const float4 co = a.conic_opacity[gid];
-            s_xy[t] = xy;
+            const uint32_t gid = a.point_list[range.x + (uint32_t)(hi - 1 - t)];
+            const float4* rec = a.records + (size_t)gid * RF4;
+            const float4 co = rec[0], r1 = rec[1];
+            s_xy[t] = make_float2(r1.x, r1.y);
             s_co[t] = co;
-            s_mask[t] = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
-            float v[NA4 * 4];
+            s_slot[t] = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
+            s_mask[t] = quadrant_mask(make_float2(r1.x, r1.y), co, tx * kTileX, ty * kTileY, a.cull);
 #pragma unroll
-            for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
-            v[0] = a.colors[3 * gid + 0];
-            v[1] = a.colors[3 * gid + 1];
-            v[2] = a.colors[3 * gid + 2];
-            v[3] = a.depths[gid];
-            const float* f = a.features + (size_t)gid * a.S;
-#pragma unroll
-            for (int c = 0; c < SMAX; ++c)
-                if (c < a.S) v[4 + c] = f[c];
-#pragma unroll
-            for (int q = 0; q < NA4; ++q)
-                s_attr[t * NA4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+            for (int q = 0; q < NA4; ++q) s_attr[t * NA4 + q] = rec[2 + q];
         }
         __syncthreads();
-        for (int j0 = 0; j0 < cnt; j0 += CH) {
-            const int jn = min(CH, cnt - j0);
-            for (int jj = 0; jj < jn; ++jj) {
-                const int j = j0 + jj;
-                const int p = hi - 1 - j;  // position in the tile range (reference `contributor`)
-                if (p >= wmax) continue;   // no pixel of this wave reaches this far back
-                const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
-                if (!((m >> w) & 1u)) continue;
-                bool contrib = inside && p < last;
-                float G = 0.f, alpha = 0.f, dx = 0.f, dy = 0.f;
-                float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (contrib) {
-                    const float2 xy = s_xy[j];
-                    co = s_co[j];
-                    dx = xy.x - pfx;
-                    dy = xy.y - pfy;
-                    const float power = gauss_power(co, dx, dy);
-                    if (power > 0.0f) {
-                        contrib = false;
-                    } else {
-                        G = __expf(power);
-                        alpha = fminf(0.99f, co.w * G);
-                        if (alpha < 1.0f / 255.0f) contrib = false;
-                    }
-                }
-                if (__ballot(contrib) == 0ull) continue;
-                float vals[NR];
-#pragma unroll
-                for (int r = 0; r < NR; ++r) vals[r] = 0.f;
-                if (contrib) {
-                    T = T / (1.f - alpha);
-                    const float dchannel_dcolor = alpha * T;
-                    float v[NA4 * 4];
-#pragma unroll
-                    for (int q = 0; q < NA4; ++q) {
-                        const float4 r = s_attr[j * NA4 + q];
-                        v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
-                    }
-                    float dL_dalpha = 0.0f;
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) {
-                        acc[c] = last_alpha * last_color[c] + (1.f - last_alpha) * acc[c];
-                        last_color[c] = v[c];
-                        dL_dalpha += (v[c] - acc[c]) * g[c];
-                        vals[kRowColor + c] = dchannel_dcolor * g[c];
-                    }
-#pragma unroll
-                    for (int c = 0; c < SMAX; ++c) {
-                        acc_f[c] = last_alpha * last_f[c] + (1.f - last_alpha) * acc_f[c];
-                        last_f[c] = v[4 + c];
-                        if (a.backward_geometry) dL_dalpha += (v[4 + c] - acc_f[c]) * gf[c];
-                        vals[kRowFeat + c] = dchannel_dcolor * gf[c];
-                    }
-                    acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
-                    last_depth = v[3];
-                    dL_dalpha += (v[3] - acc_d) * gd;
-                    acc_o = last_alpha + (1.f - last_alpha) * acc_o;
-                    dL_dalpha += (1.0f - acc_o) * go;
-                    dL_dalpha *= T;
-                    last_alpha = alpha;
-                    dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-                    const float dL_dG = co.w * dL_dalpha;
-                    const float gdx = G * dx, gdy = G * dy;
-                    const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                    const float dG_ddely = -gdy * co.z - gdx * co.y;
-                    vals[kRowMean + 0] = dL_dG * dG_ddelx * ddelx_dx;
-                    vals[kRowMean + 1] = dL_dG * dG_ddely * ddely_dy;
-                    vals[kRowMean + 2] = gd * dchannel_dcolor;
-                    vals[kRowConic + 0] = -0.5f * gdx * dx * dL_dG;
-                    vals[kRowConic + 1] = -0.5f * gdx * dy * dL_dG;
-                    vals[kRowConic + 2] = -0.5f * gdy * dy * dL_dG;
-                    vals[kRowOpacity] = G * dL_dalpha;
-                }
-                // wave totals (full exec mask here: the jj loop is wave-uniform)
-                float* dst = s_part + (w * CH + jj) * RSL;
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    if (r < kRowFeat + a.S) {
-                        const float sum = wave_sum_to_lane63(vals[r]);
-                        if (l == 63) dst[r] = sum;
-                    }
+        for (int j = 0; j < cnt; ++j) {
+            const int p = hi - 1 - j;  // position in the tile range (reference `contributor`)
+            if (p >= wmax) continue;   // no pixel of this wave reaches this far back
+            const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
+            if (!((m >> w) & 1u)) continue;
+            bool contrib = inside && p < last;
+            float G = 0.f, alpha = 0.f;
+            float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (contrib) {
+                const float2 xy = s_xy[j];
+                co = s_co[j];
+                const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
+                if (power > 0.0f) {
+                    contrib = false;
+                } else {
+                    G = __expf(power);
+                    alpha = fminf(0.99f, co.w * G);
+                    if (alpha < 1.0f / 255.0f) contrib = false;
                 }
             }
-            __syncthreads();
-            // fixed-order sum of the four wave partials -> one row per instance; re-zero
-            for (int i = t; i < jn * (RS / 4); i += kBlock) {
-                const int jj = i / (RS / 4), q = i - jj * (RS / 4);
-                float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (__ballot(contrib) == 0ull) continue;
+            float wv = 0.f, qv = 0.f;
+            if (contrib) {
+                T = T / (1.f - alpha);
+                const float dchannel_dcolor = alpha * T;
+                float v[NA4 * 4];
 #pragma unroll
-                for (int ww = 0; ww < 4; ++ww) {
-                    float4* src = s_part4 + ((ww * CH + jj) * RSL) / 4 + q;
-                    const float4 v = *src;
-                    acc4.x += v.x; acc4.y += v.y; acc4.z += v.z; acc4.w += v.w;
-                    *src = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int q = 0; q < NA4; ++q) {
+                    const float4 r = s_attr[j * NA4 + q];
+                    v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
                 }
-                reinterpret_cast<float4*>(a.rows + (size_t)s_slot[j0 + jj] * RS)[q] = acc4;
+                float dL_dalpha = 0.0f;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    acc[c] = last_alpha * last_color[c] + (1.f - last_alpha) * acc[c];
+                    last_color[c] = v[c];
+                    dL_dalpha += (v[c] - acc[c]) * g[c];
+                }
+#pragma unroll
+                for (int c = 0; c < SMAX; ++c) {
+                    acc_f[c] = last_alpha * last_f[c] + (1.f - last_alpha) * acc_f[c];
+                    last_f[c] = v[4 + c];
+                    if (a.backward_geometry) dL_dalpha += (v[4 + c] - acc_f[c]) * gf[c];
+                }
+                acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
+                last_depth = v[3];
+                dL_dalpha += (v[3] - acc_d) * gd;
+                acc_o = last_alpha + (1.f - last_alpha) * acc_o;
+                dL_dalpha += (1.0f - acc_o) * go;
+                dL_dalpha *= T;
+                last_alpha = alpha;
+                dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+                wv = dchannel_dcolor;
+                qv = G * dL_dalpha;
             }
-            __syncthreads();
+            // wave totals (full exec mask here: the j loop is wave-uniform); lane 63 writes the row
+            float* row = a.rows + ((size_t)s_slot[j] * 4 + w) * RS;
+#pragma unroll
+            for (int c = 0; c < 4 + SMAX; ++c) {
+                if (c < 4 + S) {
+                    const float gc = c < 3 ? g[c] : (c < 3 + S ? gf[c - 3 < SMAX ? c - 3 : 0] : gd);
+                    const float sum = wave_sum_to_lane63(wv * gc);
+                    if (l == 63) row[c] = sum;
+                }
+            }
+            const float mv[6] = {qv, qv * xr, qv * yr, qv * xr * xr, qv * xr * yr, qv * yr * yr};
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const float sum = wave_sum_to_lane63(mv[k]);
+                if (l == 63) row[XW + k] = sum;
+            }
+            if (l == 63) a.flags[(size_t)s_slot[j] * 4 + w] = 1;
         }
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// MFMA variant of the backward blend.
+// MFMA variant of the backward blend (default).
 //
 // Every per-pixel contribution of one instance is linear in two per-pixel scalars:
 //   w = alpha*T          -> colour (w*g_c), feature (w*gf_c) and depth (w*gd) gradients;
 //   q = G*dL_dalpha      -> opacity (q), and mean2D / conic gradients through the moments
-//                           sum q * {1, x, y, x^2, xy, y^2} of tile-centred pixel coordinates
-//                           (dx = d0x - x with d0x the centre offset; expanded at the flush).
-// So a wave's reduction over its 64 pixels for 16 instances is two small matrix products,
-// [16 inst x 64 px] @ [64 px x 16 ch], done with v_mfma_f32_16x16x4_f32 (exact f32 fma
-// chains): per 16 instances 16 MFMAs per 16-channel block instead of (10+S)*6 DPP ops per
-// instance. w and q go through a padded LDS image (row stride 66 floats: conflict-free for
-// both the row-wise writes and the column-wise A-operand reads).
+//                           sum q * {1, x, y, x^2, xy, y^2} of quadrant-centred pixel offsets
+//                           (expanded about the Gaussian's mean by the gather kernel).
+// So a wave's reduction over its 64 pixels for 16 instances is two matrix products,
+// W[16 inst x 64 px] @ X[64 px x 16 ch] and Q[16 inst x 64 px] @ Y[64 px x 16 (6 used)], each 16
+// v_mfma_f32_16x16x4_f32 (exact f32 fma chains). w and q rows go through a per-wave LDS image,
+// XOR-swizzled so the row-wise writes and the column-wise A-operand reads are conflict-free.
+//
+// Waves are independent between staging barriers: each writes its own partial row per
+// (instance, quadrant) straight from the MFMA accumulators -- no cross-wave reduction, no
+// per-chunk barriers -- and an MFMA group fills across the whole staged batch.
 // ---------------------------------------------------------------------------------------------
 
 // Order this wave's LDS traffic for cross-lane exchange through LDS: wait for the wave's DS
@@ -245,77 +215,48 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// Tuning knobs (experiment builds override them through R3DG_EXTRA_HIPFLAGS). Occupancy is
-// set by LDS and VGPRs together; the LDS allocation is rounded up in 2 KiB steps (54,020 B ran
-// at two workgroups per CU: 1.63 -> 2.09 ms). The defaults -- 128-instance staging batches and
-// a 65-float w|q row stride -- give 40,900 B (four workgroups per CU) and 127 VGPRs (four
-// waves per SIMD): 1.63 -> 1.45 ms at M1 against 256 / 66 / three waves.
+// Tuning knobs (experiment builds override them through R3DG_EXTRA_HIPFLAGS). Occupancy is set
+// by LDS and VGPRs together; the LDS allocation is rounded up in 2 KiB steps.
 #ifndef R3DG_BWD_NB
-#define R3DG_BWD_NB 128  // instances staged per batch
-#endif
-#ifndef R3DG_BWD_WQS
-#define R3DG_BWD_WQS 65  // padded LDS row stride of the w|q image
+#define R3DG_BWD_NB 64  // instances staged per batch
 #endif
 #ifndef R3DG_BWD_WAVES
 #define R3DG_BWD_WAVES 4  // waves per SIMD the register allocation targets (SMAX <= 12)
 #endif
+
+// w|q image: row r (0..15 w, 16..31 q) of 64 pixels; pixel c of row r at r*64 + (c ^ 4*(r&15)).
+// A row write (64 lanes, one row) and an A-operand read (lane l: row l&15, pixel 4*s + (l>>4)) both
+// touch 64 distinct banks.
+__device__ __forceinline__ int wq_index(int r, int c) { return r * 64 + (c ^ ((r & 15) << 2)); }
 
 template <int SMAX>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
 render_bwd_mfma_kernel(RenderBwdArgs a) {
     constexpr int NB = R3DG_BWD_NB;
     constexpr int NA4 = (4 + SMAX + 3) / 4;       // staged attribute row: colour, depth, features
-    constexpr int NR = kRowFeat + SMAX;
-    constexpr int RSL = (NR + 3) & ~3;            // LDS partial row stride (floats)
-    constexpr int CH = 32;                        // instances per flush chunk (= one compaction mask)
     constexpr int NXB = (4 + SMAX + 15) / 16;     // 16-channel blocks of X = [g0..2, gf0..S-1, gd]
-    constexpr int WQS = R3DG_BWD_WQS;             // padded LDS row stride of the w|q image
-    constexpr int GRP = 8;                        // instances per MFMA group: rows 0..7 w, 8..15 q
+    constexpr int XW = 16 * NXB;
+    constexpr int GRP = 16;                       // instances per MFMA group
     constexpr int RF4 = 2 + NA4;                  // float4s per render record in HBM
     constexpr int SF4 = 1 + NA4;                  // staged: conic|opacity, attribute row
     __shared__ float4 s_rec[NB * SF4];            // one base address per instance
     __shared__ float2 s_xy[NB];
     __shared__ uint32_t s_slot[NB];
     __shared__ uint32_t s_bits[NB / 32][4];       // [chunk][wave] live-instance masks
-    __shared__ float4 s_part4[4 * CH * RSL / 4];  // [wave][chunk instance][RSL]
-    __shared__ float s_wq[4][16 * WQS];           // per wave: rows 0..7 w, 8..15 q; [row][pixel]
-    __shared__ int s_rowid[4][GRP];
+    __shared__ float s_wq[4][2 * GRP * 64];       // per wave: w rows 0..15, q rows 16..31
+    __shared__ uint32_t s_rowslot[4][GRP];        // partial-row base (4 * slot + wave) of each group row
     __shared__ int s_max_last;
-    float* s_part = reinterpret_cast<float*>(s_part4);
 
-    const int tile = block_tile(a.tile_order, a.num_tiles);
-    if (tile >= a.num_tiles) return;
-    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
-    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
-    const bool inside = px < a.W && py < a.H;
-    const int pix = inside ? py * a.W + px : 0;
-    const float pfx = (float)px, pfy = (float)py;
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
-    const int S = a.S;
-
-    const float T_final = inside ? a.final_T[pix] : 0.f;
+    R3DG_BWD_PIXEL_SETUP()
     float T = T_final;
-    const int last = inside ? (int)a.n_contrib[pix] : 0;
-    float g[3], gf[SMAX > 0 ? SMAX : 1], gd = 0.f, go = 0.f;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) g[c] = inside ? a.dL_dpix[a.ca[c] + pix * a.cm[c]] : 0.f;
-#pragma unroll
-    for (int c = 0; c < SMAX; ++c) gf[c] = (inside && c < S) ? a.dL_dpix_f[a.gflay.a[c] + pix * a.gflay.m[c]] : 0.f;
-    if (inside) {
-        gd = a.dL_dpix_d[pix];
-        go = a.dL_dpix_o[pix];
-    }
-    const float bg_dot = a.bg[0] * g[0] + a.bg[1] * g[1] + a.bg[2] * g[2];
 
     // ---- B operands: X[pixel][channel] and Y[pixel][moment] for k-step s (pixel 4s + (l>>4)) ----
     float* wq = s_wq[w];
     float bX[NXB][16];
-    // Y[pixel][moment] = [1, x, y, x^2, xy, y^2][nch] at pixel 4*s2 + (l>>4) of this wave: its x
-    // offset depends only on s2&1 and its y offset is wave-uniform per s2, so the B operand of k-step
-    // s2 is yA[s2&1] + y*(yB[s2&1] + y*yC) (exact: every term but one is a zero product).
+    // Y[pixel][moment] = [1, x, y, x^2, xy, y^2][nch] at pixel 4*s2 + (l>>4) of this wave, offsets
+    // from the quadrant centre: x depends only on s2&1 and y = (s2>>1) - 3.5 is wave-uniform per
+    // s2, so the B operand of k-step s2 is yA[s2&1] + y*(yB[s2&1] + y*yC) (exact: every term but
+    // one is a zero product).
     float yA[2], yB[2], yC;
     {
 #pragma unroll
@@ -327,17 +268,17 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
                 if (ch < 3) v = g[ch];
                 else if (ch - 3 < SMAX && ch - 3 < S) v = gf[(ch - 3) < SMAX ? (ch - 3) : 0];
                 else if (ch == 3 + S) v = gd;
-                wq[c * WQS + l] = v;
+                wq[c * 64 + l] = v;
             }
             wave_lds_sync();
 #pragma unroll
-            for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
+            for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * 64 + 4 * s2 + (l >> 4)];
             wave_lds_sync();
         }
         const int nch = l & 15;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const float xo = (float)((w & 1) * 8 + 4 * h + (l >> 4)) - 7.5f;
+            const float xo = (float)(4 * h + (l >> 4)) - 3.5f;
             yA[h] = nch == 0 ? 1.f : (nch == 1 ? xo : (nch == 3 ? xo * xo : 0.f));
             yB[h] = nch == 2 ? 1.f : (nch == 4 ? xo : 0.f);
         }
@@ -359,32 +300,92 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     const float TFB = T_final * bg_dot;
 
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
-    if (t == 0) s_max_last = 0;
-    for (int i = t; i < 4 * CH * RSL / 4; i += kBlock) s_part4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    __syncthreads();
-    if (l == 0) atomicMax(&s_max_last, wmax);
-    __syncthreads();
-    const int max_last = s_max_last;
+    const int max_last = block_max_last(wmax, &s_max_last);
     const int RS = a.RS;
-    for (int p = max_last + t; p < n; p += kBlock) {
-        const uint32_t gid = a.point_list[range.x + p];
-        const uint32_t slot = record_slot(a.records[(size_t)gid * (2 + NA4) + 1], tx, ty, a.grid_x, a.grid_y);
-        float4* row = reinterpret_cast<float4*>(a.rows + (size_t)slot * RS);
-        for (int q = 0; q < RS / 4; ++q) row[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    // partial-row slot of each X channel / Y moment (col l&15 of the MFMA result)
     const int nch = l & 15;
-    int xslot[NXB];
-#pragma unroll
-    for (int xb = 0; xb < NXB; ++xb) {
-        const int ch = xb * 16 + nch;
-        xslot[xb] = ch < 3 ? kRowColor + ch : (ch - 3 < S ? kRowFeat + (ch - 3) : (ch == 3 + S ? kRowMean + 2 : -1));
-    }
-    // moments: S0 -> opacity slot, Sx, Sy, Sxx, Sxy, Syy -> mean x, mean y, conic x, y, w slots
-    const int yslot = nch == 0 ? kRowOpacity : (nch == 1 ? 0 : (nch == 2 ? 1 : (nch < 6 ? nch : -1)));
-    const float ctx = (float)(tx * kTileX) + 7.5f, cty = (float)(ty * kTileY) + 7.5f;
-    const bool x_half = (l >> 4) < 2;  // result rows 0..7 (w . X) live in lanes 0..31, 8..15 (q . Y) in 32..63
 
+    // One blend step of the reference's per-pixel loop (backward.cu:520-611), predicated rather
+    // than branched: every LDS read is issued up front and a non-contributing pixel (outside,
+    // past n_contrib, power > 0 or alpha < 1/255) leaves its state unchanged.
+    auto step = [&](int j, int p, bool live, float& wv, float& qv) {
+#pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
+        const int ju = __builtin_amdgcn_readfirstlane(j);  // uniform addresses
+        const float4* rj = s_rec + ju * SF4;
+        const float4 co = rj[0];
+        const float2 xy = s_xy[ju];
+        float v[NA4 * 4];
+#pragma unroll
+        for (int q = 0; q < NA4; ++q) {
+            const float4 rr = rj[1 + q];
+            v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
+        }
+        const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
+        const float G = __expf(power);
+        const float alpha = fminf(0.99f, co.w * G);
+        // p < last is false for pixels outside the image (last = 0 there)
+        const bool ok = live && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const float ae = ok ? alpha : 0.f;
+        const float Ge = ok ? G : 0.f;
+        const float rinv = __builtin_amdgcn_rcpf(1.f - ae);
+        const float Tn = T * rinv;
+#ifdef R3DG_EXP_NODOT  // timing experiment only: drop the per-pixel colour/feature dot
+        float d = go + v[0];
+#else
+        float d = __builtin_fmaf(v[0], g[0], go);
+        d = __builtin_fmaf(v[1], g[1], d);
+        d = __builtin_fmaf(v[2], g[2], d);
+        d = __builtin_fmaf(v[3], gd, d);
+#pragma unroll
+        for (int c2 = 0; c2 < SMAX; ++c2) d = __builtin_fmaf(v[4 + c2], gf[c2], d);
+#endif
+        const float diff = d - u;
+        const float dL_dalpha = rinv * __builtin_fmaf(T, diff, -TFB);
+        wv = ae * Tn;
+        qv = Ge * dL_dalpha;
+        T = Tn;
+        u = __builtin_fmaf(ae, diff, u);
+    };
+
+    // [16 w rows] x X and [16 q rows] x Y over the wave's 64 pixels; rows >= r hold stale values
+    // whose results are discarded (an output row depends on its A row only).
+    auto flush = [&](int r) {
+        if (l == 0) R3DG_EXP_ADD(1, 1);
+#ifdef R3DG_EXP_NOFLUSH  // timing experiment only: no flush products
+        return;
+#endif
+        wave_lds_sync();
+        floatx4 accX[NXB], accY = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int xb = 0; xb < NXB; ++xb) accX[xb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+            const int col = 4 * s2 + (l >> 4);
+            const float av = wq[wq_index(l & 15, col)];
+            const float aq = wq[wq_index(16 + (l & 15), col)];
+#pragma unroll
+            for (int xb = 0; xb < NXB; ++xb)
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
+            const float yo = (float)(s2 >> 1) - 3.5f;
+            const float by = yA[s2 & 1] + yo * (yB[s2 & 1] + yo * yC);
+            accY = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, by, accY, 0, 0, 0);
+        }
+        // D row 4*(l>>4)+i (group instance), column l&15 (channel / moment) -> partial row
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = (l >> 4) * 4 + i;
+            if (row < r) {
+                const uint32_t base = s_rowslot[w][row];
+                float* dst = a.rows + (size_t)base * RS;
+#pragma unroll
+                for (int xb = 0; xb < NXB; ++xb) dst[xb * 16 + nch] = accX[xb][i];
+                if (nch < 6) dst[XW + nch] = accY[i];
+                if (nch == 0) a.flags[base] = 1;
+            }
+        }
+        wave_lds_sync();
+    };
+
+    int r = 0;  // rows filled in the current MFMA group
     for (int hi = max_last; hi > 0; hi -= NB) {
         const int cnt = min(NB, hi);
         __syncthreads();
@@ -394,15 +395,15 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             const uint32_t gid = a.point_list[k];
             // one contiguous render record per Gaussian (r3dg_kernels.h record_f4), staged verbatim
             const float4* rec = a.records + (size_t)gid * RF4;
-            float4 r[RF4];
+            float4 rv[RF4];
 #pragma unroll
-            for (int q = 0; q < RF4; ++q) r[q] = rec[q];
-            s_rec[t * SF4] = r[0];
+            for (int q = 0; q < RF4; ++q) rv[q] = rec[q];
+            s_rec[t * SF4] = rv[0];
 #pragma unroll
-            for (int q = 0; q < NA4; ++q) s_rec[t * SF4 + 1 + q] = r[2 + q];
-            s_xy[t] = make_float2(r[1].x, r[1].y);
-            s_slot[t] = record_slot(r[1], tx, ty, a.grid_x, a.grid_y);
-            m = quadrant_mask(make_float2(r[1].x, r[1].y), r[0], tx * kTileX, ty * kTileY, a.cull);
+            for (int q = 0; q < NA4; ++q) s_rec[t * SF4 + 1 + q] = rv[2 + q];
+            s_xy[t] = make_float2(rv[1].x, rv[1].y);
+            s_slot[t] = record_slot(rv[1], tx, ty, a.grid_x, a.grid_y);
+            m = quadrant_mask(make_float2(rv[1].x, rv[1].y), rv[0], tx * kTileX, ty * kTileY, a.cull);
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -414,152 +415,41 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
         }
         __syncthreads();
         const int jmin = hi - wmax;  // instances j < jmin lie beyond every pixel of this wave
-        for (int c = 0; c * CH < cnt; ++c) {
+        for (int c = 0; c * 32 < cnt; ++c) {
             uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[c][w]);
-            const int lo = jmin - c * CH;
-            if (lo >= CH) bits = 0;
+            const int lo = jmin - c * 32;
+            if (lo >= 32) bits = 0;
             else if (lo > 0) bits &= ~0u << lo;
-            int r = 0;  // rows filled in the current MFMA group
-            // One blend step of the reference's per-pixel loop (backward.cu:520-611), predicated
-            // rather than branched: every LDS read is issued up front and a non-contributing pixel
-            // (outside, past n_contrib, power > 0 or alpha < 1/255) leaves its state unchanged.
-            auto step = [&](int j, bool live, float& wv, float& qv) {
-#pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
-                const int ju = __builtin_amdgcn_readfirstlane(j);  // uniform addresses
-                const float4* rj = s_rec + ju * SF4;
-                const float4 co = rj[0];
-                const float2 xy = s_xy[ju];
-                float v[NA4 * 4];
-#pragma unroll
-                for (int q = 0; q < NA4; ++q) {
-                    const float4 rr = rj[1 + q];
-                    v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
-                }
-                const int p = hi - 1 - j;  // position in the tile range (reference `contributor`)
-                const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
-                const float G = __expf(power);
-                const float alpha = fminf(0.99f, co.w * G);
-                // p < last is false for pixels outside the image (last = 0 there)
-                const bool ok = live && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-                const float ae = ok ? alpha : 0.f;
-                const float Ge = ok ? G : 0.f;
-                const float rinv = __builtin_amdgcn_rcpf(1.f - ae);
-                const float Tn = T * rinv;
-                float d = __builtin_fmaf(v[0], g[0], go);
-                d = __builtin_fmaf(v[1], g[1], d);
-                d = __builtin_fmaf(v[2], g[2], d);
-                d = __builtin_fmaf(v[3], gd, d);
-#pragma unroll
-                for (int c2 = 0; c2 < SMAX; ++c2) d = __builtin_fmaf(v[4 + c2], gf[c2], d);
-                const float diff = d - u;
-                const float dL_dalpha = rinv * __builtin_fmaf(T, diff, -TFB);
-                wv = ae * Tn;
-                qv = Ge * dL_dalpha;
-                T = Tn;
-                u = __builtin_fmaf(ae, diff, u);
-            };
+            if (l == 0) R3DG_EXP_ADD(0, __builtin_popcount(bits));
             while (bits) {
                 // two compacted instances per iteration: the second one's LDS reads and exp
                 // overlap the first one's dependent chain
-                const int jj0 = __builtin_ctz(bits);
+                const int j0 = c * 32 + __builtin_ctz(bits);
                 bits &= bits - 1;
                 const bool has1 = bits != 0u;
-                const int jj1 = has1 ? __builtin_ctz(bits) : jj0;
+                const int j1 = has1 ? c * 32 + __builtin_ctz(bits) : j0;
                 bits &= bits - 1;
                 float wv0, qv0, wv1, qv1;
-                step(c * CH + jj0, true, wv0, qv0);
-                step(c * CH + jj1, has1, wv1, qv1);
-                wq[r * WQS + l] = wv0;
-                wq[(GRP + r) * WQS + l] = qv0;
-                wq[(r + 1) * WQS + l] = wv1;
-                wq[(GRP + r + 1) * WQS + l] = qv1;
+                step(j0, hi - 1 - j0, true, wv0, qv0);
+                step(j1, hi - 1 - j1, has1, wv1, qv1);
+                wq[wq_index(r, l)] = wv0;
+                wq[wq_index(GRP + r, l)] = qv0;
+                wq[wq_index(r + 1, l)] = wv1;
+                wq[wq_index(GRP + r + 1, l)] = qv1;
                 if (l == 0) {
-                    s_rowid[w][r] = jj0;
-                    s_rowid[w][r + 1] = jj1;
+                    s_rowslot[w][r] = s_slot[j0] * 4 + w;
+                    s_rowslot[w][r + 1] = s_slot[j1] * 4 + w;
                 }
                 r += has1 ? 2 : 1;
-                if (r == GRP || bits == 0) {
-                    // [8 w rows | 8 q rows] x [64 px] against X (16 ch) and Y (moments): rows 0..7
-                    // of w.X and rows 8..15 of q.Y are the useful halves
-                    wave_lds_sync();
-                    floatx4 accX[NXB], accY = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int xb = 0; xb < NXB; ++xb) accX[xb] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int s2 = 0; s2 < 16; ++s2) {
-                        const float av = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
-#pragma unroll
-                        for (int xb = 0; xb < NXB; ++xb)
-                            accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
-                        const float yo = (float)((w >> 1) * 8 + (s2 >> 1)) - 7.5f;
-                        const float by = yA[s2 & 1] + yo * (yB[s2 & 1] + yo * yC);
-                        accY = __builtin_amdgcn_mfma_f32_16x16x4f32(av, by, accY, 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int row = (l >> 4) * 4 + i;        // D row held by this lane
-                        const int gi = x_half ? row : row - GRP;  // group instance
-                        if (gi < r) {
-                            float* dst = s_part + (w * CH + s_rowid[w][gi]) * RSL;
-                            if (x_half) {
-#pragma unroll
-                                for (int xb = 0; xb < NXB; ++xb)
-                                    if (xslot[xb] >= 0) dst[xslot[xb]] = accX[xb][i];
-                            } else if (yslot >= 0) {
-                                dst[yslot] = accY[i];
-                            }
-                        }
-                    }
-                    wave_lds_sync();
+                if (r > GRP - 2) {
+                    flush(r);
                     r = 0;
                 }
             }
-            __syncthreads();
-            // fixed-order sum of the four wave partials, moments -> mean2D / conic grads, one row
-            // per instance, re-zero the partials
-            const int jn = min(CH, cnt - c * CH);
-            constexpr int NC4 = RSL / 4;  // float4 columns; column pair 0|1 holds the moments
-            for (int it = t; it < jn * (NC4 - 1); it += kBlock) {
-                const int jj = it / (NC4 - 1);
-                const int col = it - jj * (NC4 - 1) + 1;  // 1 -> columns 0 and 1, else column col
-                const int j = c * CH + jj;
-                float4* row = reinterpret_cast<float4*>(a.rows + (size_t)s_slot[j] * RS);
-                if (col == 1) {
-                    float4 u0 = make_float4(0.f, 0.f, 0.f, 0.f), u1 = u0;
-#pragma unroll
-                    for (int ww = 0; ww < 4; ++ww) {
-                        float4* src = s_part4 + (ww * CH + jj) * NC4;
-                        const float4 v0 = src[0], v1 = src[1];
-                        u0.x += v0.x; u0.y += v0.y; u0.z += v0.z; u0.w += v0.w;
-                        u1.x += v1.x; u1.y += v1.y; u1.z += v1.z; u1.w += v1.w;
-                        src[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-                        src[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                    const float2 xy = s_xy[j];
-                    const float4 co = s_rec[j * SF4];
-                    // slots: 0 Sx, 1 Sy, 2 depth, 3 Sxx, 4 Sxy, 5 Syy, 6 S0 (= opacity grad), 7 colour r
-                    const float S0 = u1.z, Sx = u0.x, Sy = u0.y, Sxx = u0.w, Sxy = u1.x, Syy = u1.y;
-                    const float d0x = xy.x - ctx, d0y = xy.y - cty;
-                    const float Sdx = d0x * S0 - Sx, Sdy = d0y * S0 - Sy;
-                    const float Sdxdx = d0x * d0x * S0 - 2.f * d0x * Sx + Sxx;
-                    const float Sdxdy = d0x * d0y * S0 - d0x * Sy - d0y * Sx + Sxy;
-                    const float Sdydy = d0y * d0y * S0 - 2.f * d0y * Sy + Syy;
-                    row[0] = make_float4(-0.5f * a.W * co.w * (co.x * Sdx + co.y * Sdy),
-                                         -0.5f * a.H * co.w * (co.z * Sdy + co.y * Sdx), u0.z, -0.5f * co.w * Sdxdx);
-                    row[1] = make_float4(-0.5f * co.w * Sdxdy, -0.5f * co.w * Sdydy, S0, u1.w);
-                } else {
-                    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                    for (int ww = 0; ww < 4; ++ww) {
-                        float4* src = s_part4 + (ww * CH + jj) * NC4 + col;
-                        const float4 v0 = *src;
-                        u.x += v0.x; u.y += v0.y; u.z += v0.z; u.w += v0.w;
-                        *src = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                    if (4 * col < RS) row[col] = u;
-                }
-            }
-            __syncthreads();
+        }
+        if (r > 0) {  // the group's A rows and slots must not outlive this batch's staging
+            flush(r);
+            r = 0;
         }
     }
 }
@@ -815,57 +705,138 @@ __device__ __forceinline__ void gather_gaussian(const GatherBwdArgs& a, int g, c
     }
 }
 
+// Gather phase 1: per-Gaussian sums of its partial rows, in slot order then quadrant order (the
+// same fixed order every run). One group of LPG lanes per Gaussian, lane c loads float4 column c
+// of every row: c < NXC sums the X part; c == NXC expands each row's quadrant-centred moments
+// [S0, Sx, Sy, Sxx] about the Gaussian's mean (dx = mean.x - pixel.x = d0x - x with d0x =
+// mean.x - quadrant centre); c == NXC + 1 sums [Sxy, Syy], the moments whose expansion needs no
+// coefficient. Absent rows (flag byte 0) are read from the shared zero row, so every load is
+// unconditional; U slots per iteration keep U flag words and 4U row loads in flight per round
+// trip. Writes sums + g * RS = [X part (XW) | dL/dmean2D x, y | dL/dconic x, y, z | dL/dopacity
+// | 0, 0] (backward.cu:552-611 summed over the Gaussian's pixels).
+template <int SMAX>
+__global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
+    constexpr int NXB = (4 + SMAX + 15) / 16;
+    constexpr int NXC = 4 * NXB;                  // float4 columns of a partial row's X part
+    constexpr int LPG = NXC + 2 <= 8 ? 8 : 16;    // lanes per Gaussian
+    constexpr int U = 4;                          // slots per iteration
+    const int RS = a.RS;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int g = t / LPG, c = t % LPG;
+    const bool active = g < a.P && c < NXC + 2;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float S0 = 0.f, Sdx = 0.f, Sdy = 0.f, Sdxdx = 0.f, Sdxdy = 0.f, Sdydy = 0.f;
+    if (active && a.rows && a.radii[g] > 0) {
+        const uint32_t k0 = g == 0 ? 0u : a.offsets[g - 1];
+        const uint32_t k1 = a.offsets[g];
+        const float2 xy = a.means2D[g];
+        int x0, y0, x1, y1;
+        get_rect(xy.x, xy.y, a.radii[g], a.grid_x, a.grid_y, x0, y0, x1, y1);
+        const int rw = max(x1 - x0, 1);
+        int ix = 0, iy = 0;  // tile of slot kb within the Gaussian's rect (slot order = row-major rect)
+        for (uint32_t kb = k0; kb < k1; kb += U) {
+            uint32_t f[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) f[u] = kb + u < k1 ? a.flags[kb + u] : 0u;
+            float4 v[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float* row = ((f[u] >> (8 * q)) & 0xffu) ? a.rows + ((size_t)(kb + u) * 4 + q) * RS
+                                                                   : a.zero_row;
+                    v[u][q] = reinterpret_cast<const float4*>(row)[c];
+                }
+            if (c < NXC || c == NXC + 1) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        acc.x += v[u][q].x; acc.y += v[u][q].y; acc.z += v[u][q].z; acc.w += v[u][q].w;
+                    }
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const float tcx = (float)((x0 + ix) * kTileX), tcy = (float)((y0 + iy) * kTileY);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 m = v[u][q];  // S0 Sx Sy Sxx
+                        const float d0x = xy.x - (tcx + (float)((q & 1) * 8) + 3.5f);
+                        const float d0y = xy.y - (tcy + (float)((q >> 1) * 8) + 3.5f);
+                        S0 += m.x;
+                        Sdx += d0x * m.x - m.y;
+                        Sdy += d0y * m.x - m.z;
+                        Sdxdx += d0x * d0x * m.x - 2.f * d0x * m.y + m.w;
+                        Sdxdy += d0x * d0y * m.x - d0x * m.z - d0y * m.y;
+                        Sdydy += d0y * d0y * m.x - 2.f * d0y * m.z;
+                    }
+                    if (++ix == rw) {
+                        ix = 0;
+                        ++iy;
+                    }
+                }
+            }
+        }
+    }
+    // lane NXC takes the [Sxy, Syy] sums of lane NXC + 1 (all lanes take part in the shuffle)
+    const float sxy = __shfl_down(acc.x, 1), syy = __shfl_down(acc.y, 1);
+    if (!active) return;
+    float4* dst = reinterpret_cast<float4*>(a.sums + (size_t)g * RS);
+    if (c < NXC) {
+        dst[c] = acc;
+    } else if (c == NXC) {
+        Sdxdy += sxy;
+        Sdydy += syy;
+        const float4 co = a.conic_opacity[g];
+        // dL/dmean2D = -0.5 (W, H) o (o * conic . (Sdx, Sdy)), dL/dconic = -0.5 o (Sdxdx, Sdxdy,
+        // Sdydy), dL/dopacity = S0 (backward.cu:583-611)
+        dst[NXC] = make_float4(-0.5f * a.W * co.w * (co.x * Sdx + co.y * Sdy),
+                               -0.5f * a.H * co.w * (co.z * Sdy + co.y * Sdx), -0.5f * co.w * Sdxdx,
+                               -0.5f * co.w * Sdxdy);
+        dst[NXC + 1] = make_float4(-0.5f * co.w * Sdydy, S0, 0.f, 0.f);
+    }
+}
+
+// Gather phase 2: one thread per Gaussian reads its sum row, then runs the cov2D / projection /
+// SH / cov3D backward (gather_gaussian); SH coefficients staged through LDS by coalesced copies.
 template <int SMAX>
 __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     constexpr int NR = kRowFeat + SMAX;
-    constexpr int NQ = (NR + 3) / 4;       // float4 columns of a gradient row (upper bound)
-    constexpr int LPG = NQ <= 8 ? 8 : 16;  // lanes per Gaussian in the row-sum phase
+    constexpr int NXB = (4 + SMAX + 15) / 16;
+    constexpr int XW = 16 * NXB;
     constexpr int SHS = 49;                // LDS stride of one Gaussian's SH block (<= 48 used, odd)
-    constexpr int SUMF = 256 * NQ * 4, SHF = 256 * SHS;
-    __shared__ float4 s_buf4[((SUMF > SHF ? SUMF : SHF) + 3) / 4];
-    float* s_buf = reinterpret_cast<float*>(s_buf4);
+    __shared__ float s_buf[256 * SHS];
     const int t = threadIdx.x;
     const int g0 = blockIdx.x * 256;
-    const int nq = a.RS / 4;
-
-    // ---- phase 1: per-Gaussian sums of its contiguous rows. LPG lanes per Gaussian, lane c owns
-    // float4 column c, so a row is read as one contiguous 16*nq-byte segment. Rows are added in
-    // slot order, the same fixed order for every run.
-    {
-        const int c = t % LPG, gl0 = t / LPG;
-        const float4* col = reinterpret_cast<const float4*>(a.rows) + c;
-        for (int r = 0; r < LPG; ++r) {
-            const int gl = r * (256 / LPG) + gl0;
-            const int g = g0 + gl;
-            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (g < a.P && c < nq && a.radii[g] > 0) {
-                uint32_t k = g == 0 ? 0u : a.offsets[g - 1];
-                const uint32_t end = a.offsets[g];
-                for (; k + 4 <= end; k += 4) {
-                    const float4 v0 = col[(size_t)k * nq], v1 = col[(size_t)(k + 1) * nq];
-                    const float4 v2 = col[(size_t)(k + 2) * nq], v3 = col[(size_t)(k + 3) * nq];
-                    acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
-                    acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
-                    acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
-                    acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
-                }
-                for (; k < end; ++k) {
-                    const float4 v = col[(size_t)k * nq];
-                    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-                }
-            }
-            if (c < NQ) s_buf4[gl * NQ + c] = acc;
-        }
-    }
-    __syncthreads();
     const int g = g0 + t;
-    float s[NQ * 4];
+    const int S = a.S;
+
+    // sum row -> the kRow layout gather_gaussian reads
+    float s[NR];
+    if (g < a.P) {
+        const float4* src = reinterpret_cast<const float4*>(a.sums + (size_t)g * a.RS);
+        float x[XW + 8];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const float4 v = s_buf4[t * NQ + q];
-        s[4 * q] = v.x; s[4 * q + 1] = v.y; s[4 * q + 2] = v.z; s[4 * q + 3] = v.w;
+        for (int q = 0; q < XW / 4 + 2; ++q) {
+            const float4 v = src[q];
+            x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) s[kRowColor + ch] = x[ch];
+#pragma unroll
+        for (int ch = 0; ch < SMAX; ++ch) s[kRowFeat + ch] = ch < S ? x[3 + ch] : 0.f;
+        float dz = 0.f;
+#pragma unroll
+        for (int ch = 3; ch < 4 + SMAX; ++ch)
+            if (ch == 3 + S) dz = x[ch];
+        s[kRowMean + 0] = x[XW + 0];
+        s[kRowMean + 1] = x[XW + 1];
+        s[kRowMean + 2] = dz;
+        s[kRowConic + 0] = x[XW + 2];
+        s[kRowConic + 1] = x[XW + 3];
+        s[kRowConic + 2] = x[XW + 4];
+        s[kRowOpacity] = x[XW + 5];
     }
-    __syncthreads();
     // ---- SH coefficients of the block's Gaussians: one coalesced copy into LDS ----
     const int M3 = 3 * a.M;
     const int ng = min(256, a.P - g0);
@@ -891,6 +862,10 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
 
 template <int SMAX>
 static hipError_t launch_gather_s(const GatherBwdArgs& a, hipStream_t stream) {
+    constexpr int NXC = 4 * ((4 + SMAX + 15) / 16);
+    constexpr int LPG = NXC + 2 <= 8 ? 8 : 16;
+    const long long threads = (long long)a.P * LPG;
+    hipLaunchKernelGGL((row_sum_kernel<SMAX>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
     hipLaunchKernelGGL((gather_bwd_kernel<SMAX>), dim3((a.P + 255) / 256), dim3(256), 0, stream, a);
     return hipGetLastError();
 }

@@ -20,6 +20,10 @@
 
 namespace r3dg {
 
+#ifdef R3DG_EXP_COUNT
+R3DG_EXP_READER(r3dg_exp_counters_fwd)
+#endif
+
 // Tuning knobs (experiment builds override them through R3DG_EXTRA_HIPFLAGS).
 #ifndef R3DG_FWD_NB
 #define R3DG_FWD_NB 256  // instances staged per batch
@@ -141,8 +145,10 @@ render_fwd_kernel(RenderFwdArgs a) {
                     CS[1] = __builtin_fmaf(v[5], wgt, CS[1]);
                     CS[2] = __builtin_fmaf(v[6], wgt, CS[2]);
                 }
+#ifndef R3DG_EXP_NOACC  // timing experiment only: drop the feature accumulation
 #pragma unroll
                 for (int c2 = 0; c2 < SMAX; ++c2) F[c2] = __builtin_fmaf(v[FO + c2], wgt, F[c2]);
+#endif
                 Dp = __builtin_fmaf(v[3], wgt, Dp);
                 Op += wgt;
                 T = test_T;
@@ -152,6 +158,7 @@ render_fwd_kernel(RenderFwdArgs a) {
         bool alive = __ballot(!done) != 0ull;
         for (int c = 0; c < NB / 32 && alive; ++c) {
             uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[c][w]);
+            if (l == 0) R3DG_EXP_ADD(3, __builtin_popcount(bits));
             while (bits) {
 #if R3DG_FWD_PAIR
                 // two compacted instances per iteration (the second one's reads overlap the first)
@@ -162,6 +169,7 @@ render_fwd_kernel(RenderFwdArgs a) {
                 bits &= bits - 1;
                 step(j0, true);
                 step(j1, has1);
+                if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
 #else
                 const int j0 = c * 32 + __builtin_ctz(bits);
                 bits &= bits - 1;

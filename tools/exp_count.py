@@ -1,0 +1,20 @@
+"""Counting experiment (R3DG_EXP_COUNT build): one M1 step, then the device counters.
+R3DG_LIB_DIR=exp/COUNT/lib python tools/exp_count.py"""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+import relightable3dgaussian_amd as r3  # noqa: E402
+
+sys.argv = ["bench.py", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+bench.main()
+lib = ctypes.CDLL(os.path.join(r3.LIB_DIR, "libr3dg_hip.so"))
+buf, fb = (ctypes.c_ulonglong * 8)(), (ctypes.c_ulonglong * 8)()
+lib.r3dg_exp_counters_bwd(buf)
+lib.r3dg_exp_counters_fwd(fb)
+buf[2], buf[3] = fb[2], fb[3]
+names = ["bwd live pairs", "bwd mfma groups", "fwd steps done", "fwd live pairs (pre-exit)"]
+for i, n in enumerate(names):
+    print(f"{n}: {buf[i]}")
