@@ -220,14 +220,24 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef R3DG_BWD_NB
 #define R3DG_BWD_NB 64  // instances staged per batch
 #endif
+#ifndef R3DG_BWD_PKDOT
+#define R3DG_BWD_PKDOT 1  // the per-pixel channel dot as packed fp32 FMAs
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 #ifndef R3DG_BWD_WAVES
 #define R3DG_BWD_WAVES 4  // waves per SIMD the register allocation targets (SMAX <= 12)
 #endif
 
-// w|q image: row r (0..15 w, 16..31 q) of 64 pixels; pixel c of row r at r*64 + (c ^ 4*(r&15)).
-// A row write (64 lanes, one row) and an A-operand read (lane l: row l&15, pixel 4*s + (l>>4)) both
-// touch 64 distinct banks.
-__device__ __forceinline__ int wq_index(int r, int c) { return r * 64 + (c ^ ((r & 15) << 2)); }
+// w|q image: row r (0..15 w, 16..31 q) of 64 pixels, padded stride WQS = 68 floats; pixel c of
+// row r at r*WQS + c. A row write (64 lanes, one row) is 64 consecutive words, and an A-operand
+// read (lane l: row l&15, pixel 4*s + (l>>4)) hits bank 4*(l&15) + (l>>4) + 4s (mod 64): both
+// touch 64 distinct banks, and a write address is the lane base plus a wave-uniform row offset.
+constexpr int WQS = 68;
+
+// lane `lane` (wave-uniform) of v takes the wave-uniform value x (v_cmp + v_cndmask)
+__device__ __forceinline__ int write_lane(int v, int x, int lane) {
+    return (int)(threadIdx.x & 63) == lane ? x : v;
+}
 
 template <int SMAX>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
@@ -243,8 +253,7 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     __shared__ float2 s_xy[NB];
     __shared__ uint32_t s_slot[NB];
     __shared__ uint32_t s_bits[NB / 32][4];       // [chunk][wave] live-instance masks
-    __shared__ float s_wq[4][2 * GRP * 64];       // per wave: w rows 0..15, q rows 16..31
-    __shared__ uint32_t s_rowslot[4][GRP];        // partial-row base (4 * slot + wave) of each group row
+    __shared__ float s_wq[4][2 * GRP * WQS];      // per wave: w rows 0..15, q rows 16..31
     __shared__ int s_max_last;
 
     R3DG_BWD_PIXEL_SETUP()
@@ -296,8 +305,21 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
 #pragma unroll
         for (int c = 0; c < SMAX; ++c) gf[c] = 0.f;  // bX already holds the feature grads
     }
+    // upstream gradients in the staged attribute order [r, g, b, depth, f0 ..] as packed pairs
+    f32x2 gp[2 * NA4];
+#pragma unroll
+    for (int c2 = 0; c2 < 2 * NA4; ++c2) {
+        float e[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int ch = 2 * c2 + h;
+            e[h] = ch < 3 ? g[ch] : (ch == 3 ? gd : (ch - 4 < SMAX ? gf[(ch - 4) < SMAX ? ch - 4 : 0] : 0.f));
+        }
+        gp[c2] = f32x2{e[0], e[1]};
+    }
     float u = 0.f;
     const float TFB = T_final * bg_dot;
+    int rowj = 0;  // lane k: partial-row index (4 * slot + wave) of MFMA group row k
 
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
     const int max_last = block_max_last(wmax, &s_max_last);
@@ -330,6 +352,13 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
         const float Tn = T * rinv;
 #ifdef R3DG_EXP_NODOT  // timing experiment only: drop the per-pixel colour/feature dot
         float d = go + v[0];
+#elif R3DG_BWD_PKDOT
+        // packed: v_pk_fma_f32 over (channel 2c, 2c+1) pairs, two partial sums
+        f32x2 d2 = {go, 0.f};
+#pragma unroll
+        for (int c2 = 0; c2 < 2 * NA4; ++c2)
+            d2 = __builtin_elementwise_fma(f32x2{v[2 * c2], v[2 * c2 + 1]}, gp[c2], d2);
+        float d = d2.x + d2.y;
 #else
         float d = __builtin_fmaf(v[0], g[0], go);
         d = __builtin_fmaf(v[1], g[1], d);
@@ -360,8 +389,8 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
 #pragma unroll
         for (int s2 = 0; s2 < 16; ++s2) {
             const int col = 4 * s2 + (l >> 4);
-            const float av = wq[wq_index(l & 15, col)];
-            const float aq = wq[wq_index(16 + (l & 15), col)];
+            const float av = wq[(l & 15) * WQS + col];
+            const float aq = wq[(GRP + (l & 15)) * WQS + col];
 #pragma unroll
             for (int xb = 0; xb < NXB; ++xb)
                 accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
@@ -373,8 +402,8 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = (l >> 4) * 4 + i;
+            const uint32_t base = (uint32_t)__shfl(rowj, row);  // partial row of group row `row`
             if (row < r) {
-                const uint32_t base = s_rowslot[w][row];
                 float* dst = a.rows + (size_t)base * RS;
 #pragma unroll
                 for (int xb = 0; xb < NXB; ++xb) dst[xb * 16 + nch] = accX[xb][i];
@@ -432,14 +461,15 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
                 float wv0, qv0, wv1, qv1;
                 step(j0, hi - 1 - j0, true, wv0, qv0);
                 step(j1, hi - 1 - j1, has1, wv1, qv1);
-                wq[wq_index(r, l)] = wv0;
-                wq[wq_index(GRP + r, l)] = qv0;
-                wq[wq_index(r + 1, l)] = wv1;
-                wq[wq_index(GRP + r + 1, l)] = qv1;
-                if (l == 0) {
-                    s_rowslot[w][r] = s_slot[j0] * 4 + w;
-                    s_rowslot[w][r + 1] = s_slot[j1] * 4 + w;
-                }
+                float* wr = wq + r * WQS + l;
+                wr[0] = wv0;
+                wr[GRP * WQS] = qv0;
+                wr[WQS] = wv1;
+                wr[(GRP + 1) * WQS] = qv1;
+                // group row -> partial row (4 * slot + wave), kept in lane `row` of rowj: the
+                // group does not depend on the staging arrays and fills across batches
+                rowj = write_lane(rowj, (int)(s_slot[j0] * 4 + w), r);
+                rowj = write_lane(rowj, (int)(s_slot[j1] * 4 + w), r + 1);
                 r += has1 ? 2 : 1;
                 if (r > GRP - 2) {
                     flush(r);
@@ -447,11 +477,8 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
                 }
             }
         }
-        if (r > 0) {  // the group's A rows and slots must not outlive this batch's staging
-            flush(r);
-            r = 0;
-        }
     }
+    if (r > 0) flush(r);
 }
 
 template <int SMAX>
@@ -706,74 +733,77 @@ __device__ __forceinline__ void gather_gaussian(const GatherBwdArgs& a, int g, c
 }
 
 // Gather phase 1: per-Gaussian sums of its partial rows, in slot order then quadrant order (the
-// same fixed order every run). One group of LPG lanes per Gaussian, lane c loads float4 column c
-// of every row: c < NXC sums the X part; c == NXC expands each row's quadrant-centred moments
-// [S0, Sx, Sy, Sxx] about the Gaussian's mean (dx = mean.x - pixel.x = d0x - x with d0x =
-// mean.x - quadrant centre); c == NXC + 1 sums [Sxy, Syy], the moments whose expansion needs no
-// coefficient. Absent rows (flag byte 0) are read from the shared zero row, so every load is
-// unconditional; U slots per iteration keep U flag words and 4U row loads in flight per round
-// trip. Writes sums + g * RS = [X part (XW) | dL/dmean2D x, y | dL/dconic x, y, z | dL/dopacity
-// | 0, 0] (backward.cu:552-611 summed over the Gaussian's pixels).
+// same fixed order every run). One group of LPG lanes per Gaussian. The Gaussian's rows are the
+// contiguous range 4 * [k0, k1) (row 4 * slot + quadrant); per chunk of 8 slots, lanes 0..7 load
+// one flag word each and the group ORs them into a 32-bit (slot, quadrant) presence mask, then
+// walks the present rows four at a time with independent loads (absent tail rows read the shared
+// zero row). Lane c loads float4 column c of every row: c < NXC sums the X part; c == NXC expands
+// each row's quadrant-centred moments [S0, Sx, Sy, Sxx] about the Gaussian's mean (dx = mean.x -
+// pixel.x = d0x - x with d0x = mean.x - quadrant centre); c == NXC + 1 sums [Sxy, Syy], the
+// moments whose expansion needs no coefficient. Writes sums + g * RS = [X part (XW) | dL/dmean2D
+// x, y | dL/dconic x, y, z | dL/dopacity | 0, 0] (backward.cu:552-611 summed over the pixels).
 template <int SMAX>
 __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
     constexpr int NXB = (4 + SMAX + 15) / 16;
     constexpr int NXC = 4 * NXB;                  // float4 columns of a partial row's X part
     constexpr int LPG = NXC + 2 <= 8 ? 8 : 16;    // lanes per Gaussian
-    constexpr int U = 4;                          // slots per iteration
+    constexpr int CH = 8;                         // slots per chunk (one flag word per lane)
     const int RS = a.RS;
     const int t = blockIdx.x * 256 + threadIdx.x;
     const int g = t / LPG, c = t % LPG;
     const bool active = g < a.P && c < NXC + 2;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     float S0 = 0.f, Sdx = 0.f, Sdy = 0.f, Sdxdx = 0.f, Sdxdy = 0.f, Sdydy = 0.f;
-    if (active && a.rows && a.radii[g] > 0) {
-        const uint32_t k0 = g == 0 ? 0u : a.offsets[g - 1];
-        const uint32_t k1 = a.offsets[g];
-        const float2 xy = a.means2D[g];
-        int x0, y0, x1, y1;
+    uint32_t k0 = 0, n = 0;
+    float2 xy = make_float2(0.f, 0.f);
+    int x0 = 0, y0 = 0, rw = 1;
+    if (g < a.P && a.rows && a.radii[g] > 0) {  // uniform within the group
+        k0 = g == 0 ? 0u : a.offsets[g - 1];
+        n = a.offsets[g] - k0;
+        xy = a.means2D[g];
+        int x1, y1;
         get_rect(xy.x, xy.y, a.radii[g], a.grid_x, a.grid_y, x0, y0, x1, y1);
-        const int rw = max(x1 - x0, 1);
-        int ix = 0, iy = 0;  // tile of slot kb within the Gaussian's rect (slot order = row-major rect)
-        for (uint32_t kb = k0; kb < k1; kb += U) {
-            uint32_t f[U];
+        rw = max(x1 - x0, 1);
+    }
+    const float inv_rw = 1.f / (float)rw;
+    for (uint32_t kb = 0; kb < n; kb += CH) {
+        const uint32_t fw = (c < CH && kb + c < n) ? a.flags[k0 + kb + c] : 0u;
+        uint32_t mask = ((fw & 0xffu) ? 1u : 0u) | ((fw & 0xff00u) ? 2u : 0u) | ((fw & 0xff0000u) ? 4u : 0u) |
+                        ((fw & 0xff000000u) ? 8u : 0u);
+        mask <<= 4 * (c & (CH - 1));
 #pragma unroll
-            for (int u = 0; u < U; ++u) f[u] = kb + u < k1 ? a.flags[kb + u] : 0u;
-            float4 v[U][4];
+        for (int o = 1; o < LPG; o <<= 1) mask |= __shfl_xor(mask, o);
+        const float* base = a.rows + (size_t)(k0 + kb) * 4 * RS;
+        while (mask) {
+            int bit[4];
+            float4 v[4];
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float* row = ((f[u] >> (8 * q)) & 0xffu) ? a.rows + ((size_t)(kb + u) * 4 + q) * RS
-                                                                   : a.zero_row;
-                    v[u][q] = reinterpret_cast<const float4*>(row)[c];
-                }
+            for (int i = 0; i < 4; ++i) {
+                bit[i] = mask ? __builtin_ctz(mask) : 0;
+                const float* row = mask ? base + (size_t)bit[i] * RS : a.zero_row;
+                mask &= mask - 1u;
+                v[i] = active ? reinterpret_cast<const float4*>(row)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             if (c < NXC || c == NXC + 1) {
 #pragma unroll
-                for (int u = 0; u < U; ++u)
+                for (int i = 0; i < 4; ++i) {
+                    acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
+                }
+            } else if (c == NXC) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        acc.x += v[u][q].x; acc.y += v[u][q].y; acc.z += v[u][q].z; acc.w += v[u][q].w;
-                    }
-            } else {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const float tcx = (float)((x0 + ix) * kTileX), tcy = (float)((y0 + iy) * kTileY);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float4 m = v[u][q];  // S0 Sx Sy Sxx
-                        const float d0x = xy.x - (tcx + (float)((q & 1) * 8) + 3.5f);
-                        const float d0y = xy.y - (tcy + (float)((q >> 1) * 8) + 3.5f);
-                        S0 += m.x;
-                        Sdx += d0x * m.x - m.y;
-                        Sdy += d0y * m.x - m.z;
-                        Sdxdx += d0x * d0x * m.x - 2.f * d0x * m.y + m.w;
-                        Sdxdy += d0x * d0y * m.x - d0x * m.z - d0y * m.y;
-                        Sdydy += d0y * d0y * m.x - 2.f * d0y * m.z;
-                    }
-                    if (++ix == rw) {
-                        ix = 0;
-                        ++iy;
-                    }
+                for (int i = 0; i < 4; ++i) {
+                    // tile of slot kb + bit/4 in the row-major rect (slot order = duplicateWithKeys)
+                    const int idx = (int)kb + (bit[i] >> 2), q = bit[i] & 3;
+                    const int iy = (int)(((float)idx + 0.5f) * inv_rw), ix = idx - iy * rw;
+                    const float4 m = v[i];  // S0 Sx Sy Sxx (zero for the zero row)
+                    const float d0x = xy.x - ((float)((x0 + ix) * kTileX + (q & 1) * 8) + 3.5f);
+                    const float d0y = xy.y - ((float)((y0 + iy) * kTileY + (q >> 1) * 8) + 3.5f);
+                    S0 += m.x;
+                    Sdx += d0x * m.x - m.y;
+                    Sdy += d0y * m.x - m.z;
+                    Sdxdx += d0x * d0x * m.x - 2.f * d0x * m.y + m.w;
+                    Sdxdy += d0x * d0y * m.x - d0x * m.z - d0y * m.y;
+                    Sdydy += d0y * d0y * m.x - 2.f * d0y * m.z;
                 }
             }
         }

@@ -31,6 +31,9 @@ R3DG_EXP_READER(r3dg_exp_counters_fwd)
 #ifndef R3DG_FWD_WAVES
 #define R3DG_FWD_WAVES 6  // waves per SIMD the register allocation targets (SMAX <= 12)
 #endif
+#ifndef R3DG_FWD_PRED
+#define R3DG_FWD_PRED 0  // 1: accumulation predicated (weight 0) instead of branched (measured slower)
+#endif
 #ifndef R3DG_FWD_PAIR
 #define R3DG_FWD_PAIR 1  // two compacted instances per loop iteration
 #endif
@@ -135,6 +138,28 @@ render_fwd_kernel(RenderFwdArgs a) {
             const float test_T = T * (1.0f - alpha);
             const bool stop = test_T < 0.0001f;
             done = done || (contrib && stop);
+#if R3DG_FWD_PRED
+            // predicated accumulation: a non-contributing pixel adds v * 0 (exact: C + +-0 == C), so
+            // the step is straight-line code and the paired steps' LDS reads overlap
+            {
+                const bool acc = contrib && !stop;
+                const float wgt = acc ? alpha * T : 0.f;
+                C[0] = __builtin_fmaf(v[0], wgt, C[0]);
+                C[1] = __builtin_fmaf(v[1], wgt, C[1]);
+                C[2] = __builtin_fmaf(v[2], wgt, C[2]);
+                if constexpr (SHADER) {
+                    CS[0] = __builtin_fmaf(v[4], wgt, CS[0]);
+                    CS[1] = __builtin_fmaf(v[5], wgt, CS[1]);
+                    CS[2] = __builtin_fmaf(v[6], wgt, CS[2]);
+                }
+#pragma unroll
+                for (int c2 = 0; c2 < SMAX; ++c2) F[c2] = __builtin_fmaf(v[FO + c2], wgt, F[c2]);
+                Dp = __builtin_fmaf(v[3], wgt, Dp);
+                Op += wgt;
+                T = acc ? test_T : T;
+                last = acc ? (uint32_t)(base + j + 1) : last;
+            }
+#else
             if (contrib && !stop) {
                 const float wgt = alpha * T;
                 C[0] = __builtin_fmaf(v[0], wgt, C[0]);
@@ -154,6 +179,7 @@ render_fwd_kernel(RenderFwdArgs a) {
                 T = test_T;
                 last = (uint32_t)(base + j + 1);
             }
+#endif
         };
         bool alive = __ballot(!done) != 0ull;
         for (int c = 0; c < NB / 32 && alive; ++c) {
