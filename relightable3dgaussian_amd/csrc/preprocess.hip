@@ -280,10 +280,33 @@ __global__ void __launch_bounds__(256) identify_ranges_kernel(int L, const uint3
     if (idx == L - 1) ranges[cur].y = L;
 }
 
-__global__ void __launch_bounds__(256) tile_count_kernel(int T, const uint2* __restrict__ ranges,
-                                                         uint32_t* __restrict__ counts) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < T) counts[t] = ranges[t].y - ranges[t].x;
+// Backward launch order, longest tiles first: one workgroup bucket-sorts the tiles by instance
+// count (bucket = count / 4, capped; descending). Only the schedule depends on this order (each
+// tile writes its own partial rows and the gather sums them in slot order), so the order within a
+// bucket, which LDS atomics leave unspecified, does not change any result.
+__global__ void __launch_bounds__(1024) tile_order_kernel(int T, const uint2* __restrict__ ranges,
+                                                          uint32_t* __restrict__ order) {
+    constexpr int NBK = 1024;
+    __shared__ uint32_t hist[NBK];
+    __shared__ uint32_t cursor[NBK];
+    const int t = threadIdx.x;
+    hist[t] = 0;
+    __syncthreads();
+    auto bucket = [&](int tile) {
+        const uint32_t c = ranges[tile].y - ranges[tile].x;
+        return (int)min(c >> 2, (uint32_t)(NBK - 1));
+    };
+    for (int i = t; i < T; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
+    __syncthreads();
+    if (t == 0) {  // exclusive scan in descending bucket order
+        uint32_t run = 0;
+        for (int b = NBK - 1; b >= 0; --b) {
+            cursor[b] = run;
+            run += hist[b];
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < T; i += 1024) order[atomicAdd(&cursor[bucket(i)], 1u)] = (uint32_t)i;
 }
 
 }  // namespace r3dg

@@ -92,11 +92,7 @@ struct ImageState {
     float* final_T;     // [H*W]
     uint32_t* n_contrib;// [H*W]
     uint2* ranges;      // [tiles]
-    uint32_t* tile_count;        // [tiles] instances per tile
-    uint32_t* tile_count_sorted; // [tiles]
     uint32_t* tile_order;        // [tiles] tiles by descending instance count (blend launch order)
-    void* order_temp;
-    size_t order_temp_bytes;
 };
 
 size_t geom_state_bytes(size_t P, int S);

@@ -214,7 +214,7 @@ __device__ __forceinline__ int block_tile(const uint32_t* order, int num_tiles) 
     if (order) return b < num_tiles ? (int)order[b] : num_tiles;
     return xcd_tile(b, gridDim.x);
 }
-__global__ void tile_count_kernel(int T, const uint2* ranges, uint32_t* counts);
+__global__ void tile_order_kernel(int T, const uint2* ranges, uint32_t* order);
 #ifdef R3DG_EXP_COUNT  // timing/counting experiment builds only (tools/exp_build.sh)
 static __device__ unsigned long long g_exp_cnt[8];  // one copy per translation unit
 #define R3DG_EXP_READER(name)                                                        \

@@ -76,13 +76,6 @@ static size_t depth_sort_temp_size(size_t P) {  // depth sort of the Gaussians
     return bytes;
 }
 
-static size_t tile_order_temp_size(size_t T) {
-    size_t bytes = 0;
-    uint32_t* k = nullptr;
-    rocprim::radix_sort_pairs_desc(nullptr, bytes, k, k, rocprim::counting_iterator<uint32_t>(0), k, T, 0, 32, 0);
-    return bytes;
-}
-
 static bool use_tile_order() {
     const char* e = getenv("R3DG_TILE_ORDER");
     return !(e && e[0] == 'x');  // backward: "xcd" = spatial XCD-aware order; default longest first
@@ -171,11 +164,7 @@ static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end) {
     s.n_contrib = carve<uint32_t>(p, N);
     const size_t T = (size_t)num_tiles_of(H, W);
     s.ranges = carve<uint2>(p, T);
-    s.tile_count = carve<uint32_t>(p, T);
-    s.tile_count_sorted = carve<uint32_t>(p, T);
     s.tile_order = carve<uint32_t>(p, T);
-    s.order_temp_bytes = tile_order_temp_size(T);
-    s.order_temp = carve<char>(p, s.order_temp_bytes);
     if (end) *end = p;
     return s;
 }
@@ -595,11 +584,7 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     }
     const bool order_tiles = use_tile_order();
     {  // always computed (cheap), so a backward may use it whatever the forward's setting
-        hipLaunchKernelGGL(tile_count_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, img.ranges, img.tile_count);
-        size_t ob = img.order_temp_bytes;
-        R3DG_CHECK_HIP(rocprim::radix_sort_pairs_desc(img.order_temp, ob, img.tile_count, img.tile_count_sorted,
-                                                      rocprim::counting_iterator<uint32_t>(0), img.tile_order,
-                                                      (size_t)T, 0, 32, st));
+        hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, T, img.ranges, img.tile_order);
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 

@@ -391,19 +391,28 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             const int col = 4 * s2 + (l >> 4);
             const float av = wq[(l & 15) * WQS + col];
             const float aq = wq[(GRP + (l & 15)) * WQS + col];
+#ifdef R3DG_EXP_NOMFMA  // timing experiment only: A reads and stores without the products
+            accX[0][0] += av;
+            accY[0] += aq;
+#else
 #pragma unroll
             for (int xb = 0; xb < NXB; ++xb)
                 accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
             const float yo = (float)(s2 >> 1) - 3.5f;
             const float by = yA[s2 & 1] + yo * (yB[s2 & 1] + yo * yC);
             accY = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, by, accY, 0, 0, 0);
+#endif
         }
         // D row 4*(l>>4)+i (group instance), column l&15 (channel / moment) -> partial row
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = (l >> 4) * 4 + i;
             const uint32_t base = (uint32_t)__shfl(rowj, row);  // partial row of group row `row`
+#ifdef R3DG_EXP_NOSTORE  // timing experiment only: products without the row stores
+            if (row < r && a.S < 0) {
+#else
             if (row < r) {
+#endif
                 float* dst = a.rows + (size_t)base * RS;
 #pragma unroll
                 for (int xb = 0; xb < NXB; ++xb) dst[xb * 16 + nch] = accX[xb][i];
