@@ -265,6 +265,70 @@ int r3dg_texture_manager_create(int n, const char* const* names, const int64_t* 
 int r3dg_encode_texture_mode(const char* mode);
 int r3dg_encode_wrap_mode(const char* mode);
 
+/* ---- training step on the device -------------------------------------
+ * The reference keeps one nn.Parameter per attribute group and steps them with torch.optim.Adam
+ * (scene/gaussian_model.py:581-620); densification edits every group and the Adam states with
+ * boolean-mask indexing and torch.cat (gaussian_model.py:795-1062). Here all groups of one model
+ * live in ONE flat fp32 buffer: group g is a [P, width[g]] block starting at P * sum(width[<g])
+ * (the layout below), with exp_avg / exp_avg_sq buffers of the same layout. */
+#define R3DG_MAX_GROUPS 16
+typedef struct r3dg_param_layout {
+    int P;                        /* Gaussians */
+    int n_groups;                 /* <= R3DG_MAX_GROUPS */
+    int width[R3DG_MAX_GROUPS];   /* floats per Gaussian of each group */
+    int xyz, scaling, rotation, opacity; /* group index of these roles (scaling / opacity raw,
+                                             i.e. before exp / sigmoid as the reference stores them) */
+} r3dg_param_layout;
+
+/* One torch.optim.Adam step (gaussian_model.py:615-620 `step`, lr per param group) over the
+ * flat elements [lo, hi) of `param` (global indices; a rank of the sharded optimizer passes its
+ * shard). grad, exp_avg, exp_avg_sq are shard-local arrays of hi - lo floats. lr_host[g] is group
+ * g's learning rate; step is Adam's 1-based step count. Arithmetic as torch's Adam:
+ * m = lerp(m, g, 1 - b1); v = b2 v + (1 - b2) g^2; p += -(lr / (1 - b1^t)) m / (sqrt(v) /
+ * sqrt(1 - b2^t) + eps), the bias corrections in double on the host. */
+int r3dg_adam_step(const r3dg_param_layout* layout, float* param, const float* grad, float* exp_avg,
+                   float* exp_avg_sq, int64_t lo, int64_t hi, const float* lr_host, double beta1, double beta2,
+                   double eps, int step, r3dg_stream_t stream);
+
+/* train.py:172-176 + add_densification_stats (gaussian_model.py:1055-1062) for the Gaussians
+ * with radii > 0 (visibility_filter): max_radii2D = max(max_radii2D, radii); xyz_accum +=
+ * |dL/dmeans2D[:, :2]| (rows of stride2d floats); normal_accum += |normalize(normal_grad, eps=1e-3)|
+ * (skipped when normal_grad is NULL); denom += 1. */
+int r3dg_densification_stats(int P, const float* dL_dmeans2D, int stride2d, const float* normal_grad,
+                             const int* radii, float* xyz_accum, float* normal_accum, float* denom,
+                             float* max_radii2D, r3dg_stream_t stream);
+
+typedef struct r3dg_densify_args {
+    float grad_threshold, grad_normal_threshold, percent_dense, extent, min_opacity;
+    float max_screen_size; /* 0 = no screen/world size pruning (the reference's None) */
+    int N;                 /* split children per Gaussian (2) */
+    int prune_only;        /* 1: `prune` (gaussian_model.py:1045-1053), no clone / split */
+} r3dg_densify_args;
+
+/* densify_and_prune (gaussian_model.py:1025-1043; densify_and_clone :982-1023, densify_and_split
+ * :926-980, prune_points :822-848, densification_postfix :880-924) or `prune` in one device pass
+ * over the flat buffers. Result order is the reference's: surviving originals, then the clones,
+ * then the split children (child k of every split Gaussian, k = 0..N-1). max_radii2D may be
+ * NULL; as in the reference densify_and_prune's screen-size test never fires (the postfix has
+ * zeroed max_radii2D), `prune` uses it. The split samples come from `randn`: called once with
+ * n = 3 * N * n_split, it returns n standard-normal floats on the device (the reference draws
+ * torch.normal(0, std)); the new buffers come from `alloc` (param, exp_avg, exp_avg_sq, each
+ * P_new * sum(width) floats; clones and children get zero Adam state) and, when out_source is not
+ * NULL, an int32 [P_new] map: the source Gaussian of each surviving original, -1 for new rows (the
+ * caller slices its statistics with it, as prune_points does). counts = {originals kept, clones
+ * kept, Gaussians split, children kept per k}. */
+int r3dg_densify_and_prune(const r3dg_param_layout* layout, const float* param, const float* exp_avg,
+                           const float* exp_avg_sq, const float* xyz_accum, const float* normal_accum,
+                           const float* denom, const float* max_radii2D, const r3dg_densify_args* args,
+                           r3dg_alloc_fn alloc, void* alloc_ctx, r3dg_alloc_fn randn, void* randn_ctx,
+                           float** out_param, float** out_exp_avg, float** out_exp_avg_sq, int** out_source,
+                           int* P_new, int* counts, r3dg_stream_t stream);
+
+/* reset_opacity (gaussian_model.py:688-691): opacity = inverse_sigmoid(min(sigmoid(opacity), 0.01))
+ * and the opacity group's Adam state zeroed (replace_tensor_to_optimizer). */
+int r3dg_reset_opacity(const r3dg_param_layout* layout, float* param, float* exp_avg, float* exp_avg_sq,
+                       r3dg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

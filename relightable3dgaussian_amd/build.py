@@ -25,7 +25,8 @@ OBJ = os.environ.get("R3DG_OBJ_DIR") or os.path.join(PKG, "build", "obj")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
-HIP_SOURCES = ["preprocess.hip", "render_fwd.hip", "render_bwd.hip", "brdf.hip", "shaders.hip", "rasterizer.hip"]
+HIP_SOURCES = ["preprocess.hip", "render_fwd.hip", "render_bwd.hip", "brdf.hip", "shaders.hip", "rasterizer.hip",
+               "optim.hip"]
 HIP_FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
              "-munsafe-fp-atomics", f"-I{INC}", f"-I{CSRC}"]
 # the key path (projection, radius, rect) must not contract a*b+c into fma: see preprocess.hip

@@ -493,6 +493,130 @@ std::vector<int64_t> feature_groups(int64_t S) {
     return std::vector<int64_t>(g, g + n);
 }
 
+// ---- training step (include/r3dg_hip.h "training step on the device") ----
+
+r3dg_param_layout make_layout(int64_t P, const std::vector<int64_t>& widths, const std::vector<int64_t>& roles) {
+    TORCH_CHECK(!widths.empty() && widths.size() <= R3DG_MAX_GROUPS, "param layout: 1..16 groups");
+    TORCH_CHECK(roles.size() == 4, "param layout: roles = [xyz, scaling, rotation, opacity] group indices");
+    r3dg_param_layout L{};
+    L.P = (int)P;
+    L.n_groups = (int)widths.size();
+    for (size_t g = 0; g < widths.size(); ++g) L.width[g] = (int)widths[g];
+    L.xyz = (int)roles[0]; L.scaling = (int)roles[1]; L.rotation = (int)roles[2]; L.opacity = (int)roles[3];
+    return L;
+}
+
+float* f32_ptr(const torch::Tensor& t, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous(), what,
+                ": expected a contiguous float32 device tensor");
+    return t.data_ptr<float>();
+}
+
+void adam_step(int64_t P, const std::vector<int64_t>& widths, const std::vector<int64_t>& roles, torch::Tensor param,
+               const torch::Tensor& grad, torch::Tensor exp_avg, torch::Tensor exp_avg_sq, int64_t lo, int64_t hi,
+               const std::vector<double>& lrs, double beta1, double beta2, double eps, int64_t step) {
+    const r3dg_param_layout L = make_layout(P, widths, roles);
+    TORCH_CHECK(lrs.size() == widths.size(), "adam_step: one learning rate per group");
+    TORCH_CHECK(grad.numel() == hi - lo && exp_avg.numel() == hi - lo && exp_avg_sq.numel() == hi - lo,
+                "adam_step: grad / exp_avg / exp_avg_sq must hold the shard's hi - lo floats");
+    const c10::OptionalDeviceGuard guard(param.device());
+    std::vector<float> lr(lrs.begin(), lrs.end());
+    check(r3dg_adam_step(&L, f32_ptr(param, "param"), f32_ptr(grad, "grad"), f32_ptr(exp_avg, "exp_avg"),
+                         f32_ptr(exp_avg_sq, "exp_avg_sq"), lo, hi, lr.data(), beta1, beta2, eps, (int)step,
+                         stream_of(param.device())),
+          "adam_step");
+}
+
+void densification_stats(const torch::Tensor& dL_dmeans2D, const torch::Tensor& normal_grad, const torch::Tensor& radii,
+                         torch::Tensor xyz_accum, torch::Tensor normal_accum, torch::Tensor denom,
+                         torch::Tensor max_radii2D) {
+    const int P = (int)radii.size(0);
+    TORCH_CHECK(radii.scalar_type() == torch::kInt32, "densification_stats: radii must be int32");
+    TORCH_CHECK(dL_dmeans2D.dim() == 2 && dL_dmeans2D.size(0) == P && dL_dmeans2D.size(1) >= 2,
+                "densification_stats: dL_dmeans2D must be [P, >=2]");
+    TORCH_CHECK(normal_grad.numel() == 0 || normal_grad.numel() == 3 * (int64_t)P,
+                "densification_stats: normal_grad must be [P, 3] or empty");
+    const c10::OptionalDeviceGuard guard(radii.device());
+    check(r3dg_densification_stats(P, f32_ptr(dL_dmeans2D, "dL_dmeans2D"), (int)dL_dmeans2D.size(1),
+                                   normal_grad.numel() ? f32_ptr(normal_grad, "normal_grad") : nullptr,
+                                   radii.data_ptr<int>(), f32_ptr(xyz_accum, "xyz_accum"),
+                                   f32_ptr(normal_accum, "normal_accum"), f32_ptr(denom, "denom"),
+                                   f32_ptr(max_radii2D, "max_radii2D"), stream_of(radii.device())),
+          "densification_stats");
+}
+
+struct MultiAlloc {
+    torch::TensorOptions opts;
+    std::vector<torch::Tensor> ts;
+};
+void* multi_alloc(void* ctx, size_t n) {
+    auto* a = static_cast<MultiAlloc*>(ctx);
+    a->ts.push_back(torch::empty({(int64_t)std::max<size_t>((n + 3) / 4, 64)}, a->opts));
+    return a->ts.back().data_ptr();
+}
+// noise source of densify_and_split: torch.randn on the device (the reference's torch.normal)
+void* randn_alloc(void* ctx, size_t n) {
+    auto* a = static_cast<MultiAlloc*>(ctx);
+    a->ts.push_back(torch::randn({(int64_t)n}, a->opts));
+    return a->ts.back().data_ptr();
+}
+
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, int64_t, std::vector<int64_t>> densify_and_prune(
+    int64_t P, const std::vector<int64_t>& widths, const std::vector<int64_t>& roles, const torch::Tensor& param,
+    const torch::Tensor& exp_avg, const torch::Tensor& exp_avg_sq, const torch::Tensor& xyz_accum,
+    const torch::Tensor& normal_accum, const torch::Tensor& denom, const torch::Tensor& max_radii2D,
+    double grad_threshold, double grad_normal_threshold, double percent_dense, double extent, double min_opacity,
+    double max_screen_size, int64_t N, bool prune_only, const torch::Tensor& noise) {
+    const r3dg_param_layout L = make_layout(P, widths, roles);
+    const c10::OptionalDeviceGuard guard(param.device());
+    r3dg_densify_args d{};
+    d.grad_threshold = (float)grad_threshold; d.grad_normal_threshold = (float)grad_normal_threshold;
+    d.percent_dense = (float)percent_dense; d.extent = (float)extent; d.min_opacity = (float)min_opacity;
+    d.max_screen_size = (float)max_screen_size; d.N = (int)N; d.prune_only = prune_only ? 1 : 0;
+    MultiAlloc out{param.options(), {}}, rnd{param.options(), {}};
+    // a given noise tensor (tests / replicated ranks) replaces the device generator
+    auto given_noise = [](void* ctx, size_t n) -> void* {
+        auto* t = static_cast<torch::Tensor*>(ctx);
+        return (size_t)t->numel() >= n ? t->data_ptr() : nullptr;
+    };
+    torch::Tensor nz = noise;
+    float *np = nullptr, *nm = nullptr, *nv = nullptr;
+    int* src = nullptr;
+    int Pn = 0, counts[4] = {0, 0, 0, 0};
+    auto opt = [](const torch::Tensor& t, const char* w) { return t.numel() ? f32_ptr(t, w) : nullptr; };
+    check(r3dg_densify_and_prune(&L, f32_ptr(param, "param"), f32_ptr(exp_avg, "exp_avg"),
+                                 f32_ptr(exp_avg_sq, "exp_avg_sq"), opt(xyz_accum, "xyz_accum"),
+                                 opt(normal_accum, "normal_accum"), opt(denom, "denom"),
+                                 opt(max_radii2D, "max_radii2D"), &d, multi_alloc, &out,
+                                 noise.numel() ? (r3dg_alloc_fn)given_noise : randn_alloc,
+                                 noise.numel() ? (void*)&nz : (void*)&rnd, &np, &nm, &nv, &src, &Pn, counts,
+                                 stream_of(param.device())),
+          "densify_and_prune");
+    auto find = [&](void* p) {
+        for (auto& t : out.ts)
+            if (t.data_ptr() == p) return t;
+        TORCH_CHECK(false, "densify_and_prune: output not found");
+        return torch::Tensor();
+    };
+    int64_t W = 0;
+    for (auto w : widths) W += w;
+    const int64_t n = (int64_t)Pn * W;
+    torch::Tensor source = torch::from_blob(src, {(int64_t)Pn}, [](void*) {}, param.options().dtype(torch::kInt32));
+    source = source.clone();  // own the map (the scratch allocation is released on return)
+    return {find(np).narrow(0, 0, n), find(nm).narrow(0, 0, n), find(nv).narrow(0, 0, n), source, (int64_t)Pn,
+            std::vector<int64_t>{counts[0], counts[1], counts[2], counts[3]}};
+}
+
+void reset_opacity(int64_t P, const std::vector<int64_t>& widths, const std::vector<int64_t>& roles,
+                   torch::Tensor param, const torch::Tensor& exp_avg, const torch::Tensor& exp_avg_sq) {
+    const r3dg_param_layout L = make_layout(P, widths, roles);
+    const c10::OptionalDeviceGuard guard(param.device());
+    check(r3dg_reset_opacity(&L, f32_ptr(param, "param"), exp_avg.numel() ? f32_ptr(exp_avg, "exp_avg") : nullptr,
+                             exp_avg_sq.numel() ? f32_ptr(exp_avg_sq, "exp_avg_sq") : nullptr,
+                             stream_of(param.device())),
+          "reset_opacity");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -520,6 +644,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("create_shader_manager", &create_shader_manager);
     m.def("shader_manager_info", &shader_manager_info);
     m.def("abi_version", []() { return r3dg_abi_version(); });
+    // training step on the device (§8f rank 3)
+    m.def("adam_step", &adam_step);
+    m.def("densification_stats", &densification_stats);
+    m.def("densify_and_prune", &densify_and_prune);
+    m.def("reset_opacity", &reset_opacity);
     m.def("profile_enable", [](int64_t n) { check(r3dg_profile_enable((int)n), "profile_enable"); });
     m.def("profile_read", [](int64_t kernel) {
         int c = 0;
