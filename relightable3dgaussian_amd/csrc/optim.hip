@@ -211,57 +211,58 @@ __device__ __forceinline__ void rotation_matrix(const float* q4, float R[3][3]) 
     R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
 }
 
-// One thread per source Gaussian writes its surviving rows of every group and of both Adam states.
-__global__ void __launch_bounds__(256) densify_scatter_kernel(DensifyArgs a) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.P) return;
+// One thread per (group, Gaussian, element) of the source buffer -- consecutive threads touch
+// consecutive floats of a group, so every read and write is coalesced -- writes that float of
+// the Gaussian's surviving rows: original, clone, and the N split children.
+__global__ void __launch_bounds__(256) densify_scatter_kernel(DensifyArgs a, long long total) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (t >= total) return;
+    int g = 0;
+    while (g < a.n_groups - 1 && t >= a.off[g + 1]) ++g;
+    const int w = a.width[g];
+    const long long local = t - a.off[g];
+    const int i = (int)(local / w), e = (int)(local - (long long)i * w);
     const uint4 c = a.codes[i], p = a.pos[i];
+    if (!(c.x | c.y | c.z)) return;
     const long long nO = a.tot.x, nC = a.tot.y, nS = a.tot.z, nSplit = a.tot.w;
-    const long long rowO = p.x, rowC = nO + p.y;
-    auto copy_row = [&](int g, long long dst_row, bool zero_state) {
-        const int w = a.width[g];
-        const float* src = a.param + a.off[g] + (size_t)i * w;
-        const long long d = a.noff[g] + dst_row * w;
-        for (int e = 0; e < w; ++e) {
-            a.out_param[d + e] = src[e];
-            a.out_m[d + e] = zero_state ? 0.f : a.m[a.off[g] + (size_t)i * w + e];
-            a.out_v[d + e] = zero_state ? 0.f : a.v[a.off[g] + (size_t)i * w + e];
-        }
-    };
-    for (int g = 0; g < a.n_groups; ++g) {
-        if (c.x) copy_row(g, rowO, false);
-        if (c.y) copy_row(g, rowC, true);  // cat_tensors_to_optimizer: zero state for new rows
+    const float val = a.param[t];
+    if (c.x) {
+        const long long d = a.noff[g] + (long long)p.x * w + e;
+        a.out_param[d] = val;
+        a.out_m[d] = a.m[t];
+        a.out_v[d] = a.v[t];
+        if (a.out_source && g == 0 && e == 0) a.out_source[p.x] = i;
     }
-    if (a.out_source) {
-        if (c.x) a.out_source[rowO] = i;
-        if (c.y) a.out_source[rowC] = -1;
+    if (c.y) {  // clone (densify_and_clone :993-1023): copied values, zero Adam state
+        const long long d = a.noff[g] + (nO + p.y) * w + e;
+        a.out_param[d] = val;
+        a.out_m[d] = 0.f;
+        a.out_v[d] = 0.f;
+        if (a.out_source && g == 0 && e == 0) a.out_source[nO + p.y] = -1;
     }
     if (!c.z) return;
     // split children (densify_and_split :940-954): xyz = R(q) (std * z) + xyz, scaling =
     // log(exp(s) / (0.8 N)), every other group copied; child k of split rank r takes noise row
     // k * nSplit + r (torch.normal over the .repeat(N, 1) stack)
-    const float* xyz = a.param + a.off[a.gxyz] + 3 * (size_t)i;
     const float* sc = a.param + a.off[a.gscale] + 3 * (size_t)i;
-    float R[3][3];
-    rotation_matrix(a.param + a.off[a.grot] + 4 * (size_t)i, R);
-    const float std3[3] = {expf(sc[0]), expf(sc[1]), expf(sc[2])};
-    const float div = 0.8f * (float)a.d.N;
     for (int k = 0; k < a.d.N; ++k) {
         const long long row = nO + nC + (long long)k * nS + p.z;
-        if (a.out_source) a.out_source[row] = -1;
-        const float* z = a.noise + 3 * ((size_t)k * nSplit + p.w);
-        float smp[3];
-        for (int r = 0; r < 3; ++r) smp[r] = 0.f + std3[r] * z[r];
-        for (int g = 0; g < a.n_groups; ++g) {
-            copy_row(g, row, true);
-            const long long d = a.noff[g] + row * a.width[g];
-            if (g == a.gxyz) {
-                for (int r = 0; r < 3; ++r)
-                    a.out_param[d + r] = R[r][0] * smp[0] + R[r][1] * smp[1] + R[r][2] * smp[2] + xyz[r];
-            } else if (g == a.gscale) {
-                for (int r = 0; r < 3; ++r) a.out_param[d + r] = logf(std3[r] / div);
-            }
+        float out = val;
+        if (g == a.gxyz) {
+            float R[3][3];
+            rotation_matrix(a.param + a.off[a.grot] + 4 * (size_t)i, R);
+            const float* z = a.noise + 3 * ((size_t)k * nSplit + p.w);
+            float smp[3];
+            for (int r = 0; r < 3; ++r) smp[r] = 0.f + expf(sc[r]) * z[r];
+            out = R[e][0] * smp[0] + R[e][1] * smp[1] + R[e][2] * smp[2] + val;
+        } else if (g == a.gscale) {
+            out = logf(expf(val) / (0.8f * (float)a.d.N));
         }
+        const long long d = a.noff[g] + row * w + e;
+        a.out_param[d] = out;
+        a.out_m[d] = 0.f;
+        a.out_v[d] = 0.f;
+        if (a.out_source && g == 0 && e == 0) a.out_source[row] = -1;
     }
 }
 
@@ -394,7 +395,8 @@ extern "C" int r3dg_densify_and_prune(const r3dg_param_layout* L, const float* p
         R3DG_REQUIRE(a.noise, "densify: noise source failed");
     }
     if (P > 0) {
-        hipLaunchKernelGGL(densify_scatter_kernel, dim3((P + 255) / 256), dim3(256), 0, st, a);
+        const long long total = (long long)P * W;
+        hipLaunchKernelGGL(densify_scatter_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a, total);
         R3DG_CHECK_HIP(hipGetLastError());
     }
     *out_param = a.out_param; *out_exp_avg = a.out_m; *out_exp_avg_sq = a.out_v;
