@@ -5,16 +5,20 @@
 //
 // MI355X design (replaces the reference's per-pixel float atomicAdd scatter, ~(10+S) atomics
 // per contributing pixel, backward.cu:552-611):
-//   1. render_bwd_kernel: one workgroup per tile replays the tile's list back to front. For each
-//      instance every wave reduces its 64 pixels' contributions with DPP (6 VALU ops per value,
-//      no LDS traffic) and lane 63 stores the wave total in the wave's own LDS partial row; per
-//      chunk of 64 instances the block sums the four wave partials in a fixed order and writes
-//      ONE gradient row per (tile, Gaussian) instance with plain vector stores -- at the
-//      instance's unsorted slot, which the sort permutation gives us. Slots are
-//      Gaussian-contiguous (duplicateWithKeys order).
-//   2. gather_bwd_kernel: one thread per Gaussian sums its contiguous rows in a fixed order,
-//      then runs the cov2D / projection / SH / cov3D backward for that Gaussian. No global
-//      atomics anywhere; the result is bitwise reproducible run to run (the reference's is not).
+//   1. render_bwd_mfma_kernel: one workgroup per tile (longest tiles first) replays the tile's
+//      list back to front; wave w owns the tile's 8x8 quadrant w. Per live (instance, wave) pair
+//      a predicated blend step yields two per-pixel scalars w = alpha*T and q = G*dL/dalpha; the
+//      wave's 64-pixel reductions of 16 instances are two MFMA products (w x [colour, feature,
+//      depth grads], q x pixel moments) whose results go straight from the accumulators to one
+//      partial row per (instance, quadrant) at index 4 * slot + quadrant, flagged -- no
+//      cross-wave reduction, no per-chunk barriers. render_bwd_dpp_kernel is the DPP-reduction
+//      cross-check (R3DG_BWD=dpp) writing the same rows.
+//   2. row_sum_kernel: one 8-lane group per Gaussian sums its flagged partial rows (contiguous:
+//      slots are Gaussian-major, duplicateWithKeys order) in a fixed order and expands the
+//      quadrant-centred moments into the mean2D / conic / opacity gradients.
+//   3. gather_bwd_kernel: one thread per Gaussian runs the cov2D / projection / SH / cov3D
+//      backward. No global atomics anywhere: gradients are bitwise reproducible run to run (the
+//      reference's are not).
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
 
