@@ -180,6 +180,19 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));    // packed fp32 pair 
 // Exponent of the 2D Gaussian at offset (dx, dy) from its centre: -0.5 (a dx^2 + c dy^2) - b dx dy
 // (forward.cu:478, backward.cu:530). One fixed FMA pattern, so every call site -- forward and
 // backward, first or second instance of an unrolled pair -- rounds identically.
+// The blend kernels stage each instance's conic in the exp2 domain once, so a per-pixel step
+// evaluates power * log2(e) = dx (A dx + B dy) + C dy^2 in 5 VALU ops and feeds v_exp_f32
+// directly (A = -log2(e)/2 a, B = -log2(e) b, C = -log2(e)/2 c): 3 fewer ops than gauss_power
+// followed by __expf. The sign tests (power > 0) are unchanged by the positive scale.
+__device__ __forceinline__ float4 exp2_conic(float4 co) {
+    constexpr float L2E = 1.4426950408889634f;
+    return make_float4(-0.5f * L2E * co.x, -L2E * co.y, -0.5f * L2E * co.z, co.w);
+}
+__device__ __forceinline__ float gauss_power2(float4 k, float dx, float dy) {
+#pragma clang fp contract(off)
+    return __builtin_fmaf(k.z * dy, dy, dx * __builtin_fmaf(k.y, dy, k.x * dx));
+}
+
 __device__ __forceinline__ float gauss_power(float4 co, float dx, float dy) {
 #pragma clang fp contract(off)
     const float q = __builtin_fmaf(co.x * dx, dx, (co.z * dy) * dy);

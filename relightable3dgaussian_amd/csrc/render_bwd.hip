@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
             const float4* rec = a.records + (size_t)gid * RF4;
             const float4 co = rec[0], r1 = rec[1];
             s_xy[t] = make_float2(r1.x, r1.y);
-            s_co[t] = co;
+            s_co[t] = exp2_conic(co);
             s_slot[t] = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
             s_mask[t] = quadrant_mask(make_float2(r1.x, r1.y), co, tx * kTileX, ty * kTileY, a.cull);
 #pragma unroll
@@ -129,11 +129,11 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
             if (contrib) {
                 const float2 xy = s_xy[j];
                 co = s_co[j];
-                const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
+                const float power = gauss_power2(co, xy.x - pfx, xy.y - pfy);  // exp2-domain conic
                 if (power > 0.0f) {
                     contrib = false;
                 } else {
-                    G = __expf(power);
+                    G = __builtin_amdgcn_exp2f(power);
                     alpha = fminf(0.99f, co.w * G);
                     if (alpha < 1.0f / 255.0f) contrib = false;
                 }
@@ -232,11 +232,13 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #define R3DG_BWD_WAVES 4  // waves per SIMD the register allocation targets (SMAX <= 12)
 #endif
 
-// w|q image: row r (0..15 w, 16..31 q) of 64 pixels, padded stride WQS = 68 floats; pixel c of
-// row r at r*WQS + c. A row write (64 lanes, one row) is 64 consecutive words, and an A-operand
-// read (lane l: row l&15, pixel 4*s + (l>>4)) hits bank 4*(l&15) + (l>>4) + 4s (mod 64): both
-// touch 64 distinct banks, and a write address is the lane base plus a wave-uniform row offset.
-constexpr int WQS = 68;
+// w|q image: row r (0..15 w, 16..31 q) of 64 pixels, padded stride WQS = 66 floats; pixel c of
+// row r at r*WQS + c. ds_read_b32 / ds_write_b32 bank by dword address mod 32 within each 32-lane
+// half (MI355X_MICROARCH.md §LDS): a row write is 32 consecutive dwords per half, and an
+// A-operand read (lane l: row l&15, pixel 4*s + (l>>4)) hits bank 2*(l&15) + (l>>4) + 4s (mod 32),
+// 32 distinct banks per half -- both conflict-free (stride 64 or 68 would be 16- / 2-way) -- and a
+// write address is the lane base plus a wave-uniform row offset.
+constexpr int WQS = 66;
 
 // lane `lane` (wave-uniform) of v takes the wave-uniform value x (v_cmp + v_cndmask)
 __device__ __forceinline__ int write_lane(int v, int x, int lane) {
@@ -281,11 +283,11 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
                 if (ch < 3) v = g[ch];
                 else if (ch - 3 < SMAX && ch - 3 < S) v = gf[(ch - 3) < SMAX ? (ch - 3) : 0];
                 else if (ch == 3 + S) v = gd;
-                wq[c * 64 + l] = v;
+                wq[c * WQS + l] = v;
             }
             wave_lds_sync();
 #pragma unroll
-            for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * 64 + 4 * s2 + (l >> 4)];
+            for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
             wave_lds_sync();
         }
         const int nch = l & 15;
@@ -345,8 +347,8 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             const float4 rr = rj[1 + q];
             v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
         }
-        const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
-        const float G = __expf(power);
+        const float power = gauss_power2(co, xy.x - pfx, xy.y - pfy);  // exp2-domain conic
+        const float G = __builtin_amdgcn_exp2f(power);
         const float alpha = fminf(0.99f, co.w * G);
         // p < last is false for pixels outside the image (last = 0 there)
         const bool ok = live && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
@@ -440,7 +442,7 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             float4 rv[RF4];
 #pragma unroll
             for (int q = 0; q < RF4; ++q) rv[q] = rec[q];
-            s_rec[t * SF4] = rv[0];
+            s_rec[t * SF4] = exp2_conic(rv[0]);
 #pragma unroll
             for (int q = 0; q < NA4; ++q) s_rec[t * SF4 + 1 + q] = rv[2 + q];
             s_xy[t] = make_float2(rv[1].x, rv[1].y);

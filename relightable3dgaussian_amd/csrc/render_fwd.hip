@@ -46,7 +46,8 @@ render_fwd_kernel(RenderFwdArgs a) {
     constexpr int NA4 = (FO + SMAX + 3) / 4;           // float4 per attribute row
     __shared__ float2 s_xy[NB];
     __shared__ float4 s_co[NB];
-    __shared__ float4 s_attr[NB * NA4];
+    __shared__ float4 s_attr[NA4 * NB];                // q-major: float4 q of instance j at q*NB + j
+                                                       // (staging writes 16-B strided: conflict-free)
     __shared__ uint32_t s_bits[NB / 32][4];            // [32-instance chunk][wave]: live-instance masks
 
     const int tile = block_tile(a.tile_order, a.num_tiles);
@@ -79,15 +80,15 @@ render_fwd_kernel(RenderFwdArgs a) {
                 const float4 co = rec[0], r1 = rec[1];
                 const float2 xy = make_float2(r1.x, r1.y);
                 s_xy[t] = xy;
-                s_co[t] = co;
+                s_co[t] = exp2_conic(co);
                 m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
 #pragma unroll
-                for (int q = 0; q < NA4; ++q) s_attr[t * NA4 + q] = rec[2 + q];
+                for (int q = 0; q < NA4; ++q) s_attr[q * NB + t] = rec[2 + q];
             } else {
                 const float2 xy = a.means2D[gid];
                 const float4 co = a.conic_opacity[gid];
                 s_xy[t] = xy;
-                s_co[t] = co;
+                s_co[t] = exp2_conic(co);
                 m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
                 float v[NA4 * 4];
 #pragma unroll
@@ -107,7 +108,7 @@ render_fwd_kernel(RenderFwdArgs a) {
                     if (c < a.S) v[FO + c] = f[c];
 #pragma unroll
                 for (int q = 0; q < NA4; ++q)
-                    s_attr[t * NA4 + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                    s_attr[q * NB + t] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
             }
         }
         // compaction: this wave's 64 staged slots are chunks 2w and 2w+1; one ballot per target wave
@@ -129,11 +130,11 @@ render_fwd_kernel(RenderFwdArgs a) {
             float v[NA4 * 4];
 #pragma unroll
             for (int q = 0; q < NA4; ++q) {
-                const float4 r = s_attr[j * NA4 + q];
+                const float4 r = s_attr[q * NB + j];
                 v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
             }
-            const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
-            const float alpha = fminf(0.99f, co.w * __expf(power));
+            const float power = gauss_power2(co, xy.x - pfx, xy.y - pfy);  // exp2-domain conic
+            const float alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(power));
             const bool contrib = live && !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
             const float test_T = T * (1.0f - alpha);
             const bool stop = test_T < 0.0001f;

@@ -20,7 +20,8 @@ def pick(prefix):
 
 out = {"config": config, "source": src, "method": "FETCH_SIZE*2 + WRITE_SIZE (KiB*1024), mean per launch"}
 for name, prefix in [("render_fwd", "render_fwd_kernel"), ("render_bwd", "render_bwd_mfma_kernel"),
-                     ("gather_bwd", "gather_bwd_kernel"), ("preprocess", "preprocess_kernel")]:
+                     ("row_sum", "row_sum_kernel"), ("gather_bwd", "gather_bwd_kernel"),
+                     ("preprocess", "preprocess_kernel")]:
     k, v = pick(prefix)
     out[name + "_kernel"] = k
     out[name + "_bytes"] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))
