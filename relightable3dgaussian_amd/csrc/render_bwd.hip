@@ -39,8 +39,12 @@ __device__ __forceinline__ int wave_max_int(int v) {
 #define R3DG_BWD_PIXEL_SETUP()                                                                          \
     const int tile = block_tile(a.tile_order, a.num_tiles);                                             \
     if (tile >= a.num_tiles) return;                                                                    \
-    const int tx = tile % a.grid_x, ty = tile / a.grid_x;                                               \
     const int t = threadIdx.x, w = t >> 6, l = t & 63;                                                  \
+    R3DG_BWD_PIXELS()
+
+// Pixel (l & 7, l >> 3) of quadrant w of `tile` and its upstream gradients (tile, w, l defined).
+#define R3DG_BWD_PIXELS()                                                                               \
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;                                               \
     const int px = tx * kTileX + (w & 1) * 8 + (l & 7);                                                 \
     const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);                                               \
     const bool inside = px < a.W && py < a.H;                                                           \
@@ -245,10 +249,21 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
-template <int SMAX>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
+#ifndef R3DG_BWDW_NB
+#define R3DG_BWDW_NB 32  // instances staged per batch by a one-wave workgroup
+#endif
+
+// PW = false: one 256-thread workgroup per tile, wave w = quadrant w, staging shared by the four
+// waves (two block barriers per batch). PW = true: one 64-thread workgroup per (tile, quadrant),
+// staging private to the wave, no block barriers -- a wave never waits for the other quadrants of
+// its tile (their live-instance counts and n_contrib depths differ widely) and iterates only up to
+// its own n_contrib maximum. The four quadrant workgroups of a tile are blocks b, b+8, b+16, b+24,
+// so they share an XCD (and its L2 copy of the tile's render records).
+template <int SMAX, bool PW>
+__global__ void __launch_bounds__(PW ? 64 : kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
 render_bwd_mfma_kernel(RenderBwdArgs a) {
-    constexpr int NB = R3DG_BWD_NB;
+    constexpr int NB = PW ? R3DG_BWDW_NB : R3DG_BWD_NB;
+    constexpr int NW = PW ? 1 : 4;                // waves per workgroup
     constexpr int NA4 = (4 + SMAX + 3) / 4;       // staged attribute row: colour, depth, features
     constexpr int NXB = (4 + SMAX + 15) / 16;     // 16-channel blocks of X = [g0..2, gf0..S-1, gd]
     constexpr int XW = 16 * NXB;
@@ -258,15 +273,28 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     __shared__ float4 s_rec[NB * SF4];            // one base address per instance
     __shared__ float2 s_xy[NB];
     __shared__ uint32_t s_slot[NB];
-    __shared__ uint32_t s_bits[NB / 32][4];       // [chunk][wave] live-instance masks
-    __shared__ float s_wq[4][2 * GRP * WQS];      // per wave: w rows 0..15, q rows 16..31
+    __shared__ uint32_t s_bits[PW ? 1 : NB / 32][4];  // [chunk][wave] live-instance masks (PW: unused)
+    __shared__ float s_wq[NW][2 * GRP * WQS];     // per wave: w rows 0..15, q rows 16..31
     __shared__ int s_max_last;
 
-    R3DG_BWD_PIXEL_SETUP()
+    int tile, w;
+    if constexpr (PW) {
+        const int b = blockIdx.x, xcd = b & 7, k = b >> 3;
+        w = k & 3;
+        const int vb = ((k >> 2) << 3) | xcd;  // this tile's position in the tile launch order
+        tile = a.tile_order ? (vb < a.num_tiles ? (int)a.tile_order[vb] : a.num_tiles)
+                            : xcd_tile(vb, (int)gridDim.x >> 2);
+    } else {
+        tile = block_tile(a.tile_order, a.num_tiles);
+        w = threadIdx.x >> 6;
+    }
+    if (tile >= a.num_tiles) return;
+    const int t = threadIdx.x, l = t & 63;
+    R3DG_BWD_PIXELS()
     float T = T_final;
 
     // ---- B operands: X[pixel][channel] and Y[pixel][moment] for k-step s (pixel 4s + (l>>4)) ----
-    float* wq = s_wq[w];
+    float* wq = s_wq[PW ? 0 : w];
     float bX[NXB][16];
     // Y[pixel][moment] = [1, x, y, x^2, xy, y^2][nch] at pixel 4*s2 + (l>>4) of this wave, offsets
     // from the quadrant centre: x depends only on s2&1 and y = (s2>>1) - 3.5 is wave-uniform per
@@ -328,7 +356,7 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     int rowj = 0;  // lane k: partial-row index (4 * slot + wave) of MFMA group row k
 
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
-    const int max_last = block_max_last(wmax, &s_max_last);
+    const int max_last = PW ? wmax : block_max_last(wmax, &s_max_last);
     const int RS = a.RS;
     const int nch = l & 15;
 
@@ -430,18 +458,30 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     };
 
     int r = 0;  // rows filled in the current MFMA group
+#ifdef R3DG_EXP_COUNT
+    const long long t_begin = wall_clock64();
+    long long t_stage = 0;
+#endif
+    // Gaussian ids of the next batch, loaded one batch ahead: staging then waits for one
+    // dependent memory round trip (the render records) instead of two
+    uint32_t gid_next = t < min(NB, max_last) ? a.point_list[range.x + (uint32_t)(max_last - 1 - t)] : 0u;
     for (int hi = max_last; hi > 0; hi -= NB) {
         const int cnt = min(NB, hi);
-        __syncthreads();
+#ifdef R3DG_EXP_COUNT
+        const long long ts0 = wall_clock64();
+#endif
+        if constexpr (PW) wave_lds_sync();  // this wave's reads of the previous batch are done
+        else __syncthreads();
         uint32_t m = 0;
         if (t < cnt) {
-            const uint32_t k = range.x + (uint32_t)(hi - 1 - t);
-            const uint32_t gid = a.point_list[k];
+            const uint32_t gid = gid_next;
             // one contiguous render record per Gaussian (r3dg_kernels.h record_f4), staged verbatim
             const float4* rec = a.records + (size_t)gid * RF4;
             float4 rv[RF4];
 #pragma unroll
             for (int q = 0; q < RF4; ++q) rv[q] = rec[q];
+            const int hn = hi - NB;
+            gid_next = (hn > 0 && t < min(NB, hn)) ? a.point_list[range.x + (uint32_t)(hn - 1 - t)] : 0u;
             s_rec[t * SF4] = exp2_conic(rv[0]);
 #pragma unroll
             for (int q = 0; q < NA4; ++q) s_rec[t * SF4 + 1 + q] = rv[2 + q];
@@ -449,18 +489,27 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             s_slot[t] = record_slot(rv[1], tx, ty, a.grid_x, a.grid_y);
             m = quadrant_mask(make_float2(rv[1].x, rv[1].y), rv[0], tx * kTileX, ty * kTileY, a.cull);
         }
+        unsigned long long live = 0;  // PW: this quadrant's live instances of the batch
+        if constexpr (PW) {
+            live = __ballot((m >> w) & 1u);
+            wave_lds_sync();
+        } else {
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const unsigned long long bal = __ballot((m >> b) & 1u);
-            if (l == 0 && w < NB / 64) {
-                s_bits[2 * w][b] = (uint32_t)bal;
-                s_bits[2 * w + 1][b] = (uint32_t)(bal >> 32);
+            for (int b = 0; b < 4; ++b) {
+                const unsigned long long bal = __ballot((m >> b) & 1u);
+                if (l == 0 && w < NB / 64) {
+                    s_bits[2 * w][b] = (uint32_t)bal;
+                    s_bits[2 * w + 1][b] = (uint32_t)(bal >> 32);
+                }
             }
+            __syncthreads();
         }
-        __syncthreads();
+#ifdef R3DG_EXP_COUNT
+        t_stage += wall_clock64() - ts0;
+#endif
         const int jmin = hi - wmax;  // instances j < jmin lie beyond every pixel of this wave
         for (int c = 0; c * 32 < cnt; ++c) {
-            uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[c][w]);
+            uint32_t bits = PW ? (uint32_t)(live >> (32 * c)) : __builtin_amdgcn_readfirstlane(s_bits[c][w]);
             const int lo = jmin - c * 32;
             if (lo >= 32) bits = 0;
             else if (lo > 0) bits &= ~0u << lo;
@@ -494,18 +543,26 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
         }
     }
     if (r > 0) flush(r);
+#ifdef R3DG_EXP_COUNT
+    if (l == 0) {
+        R3DG_EXP_ADD(2, t_stage);                   // staging + its two barriers, per wave
+        R3DG_EXP_ADD(3, wall_clock64() - t_begin);  // batch loop total, per wave
+    }
+#endif
 }
 
 template <int SMAX>
 static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
-    const char* e = getenv("R3DG_BWD");  // "dpp" selects the DPP-reduction variant (A/B and cross-check)
-    const bool use_dpp = e && e[0] == 'd';
-    if (use_dpp)
-        hipLaunchKernelGGL((render_bwd_dpp_kernel<SMAX>), dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0, stream,
-                           a);
+    // R3DG_BWD: "dpp" = DPP-reduction cross-check, "wave" = one 64-thread workgroup per (tile,
+    // quadrant) (measured 7 % slower at M1), default = one 256-thread workgroup per tile
+    const char* e = getenv("R3DG_BWD");
+    const int grid = padded_tile_grid(a.num_tiles);
+    if (e && e[0] == 'd')
+        hipLaunchKernelGGL((render_bwd_dpp_kernel<SMAX>), dim3(grid), dim3(kBlock), 0, stream, a);
+    else if (e && e[0] == 'w')
+        hipLaunchKernelGGL((render_bwd_mfma_kernel<SMAX, true>), dim3(4 * grid), dim3(64), 0, stream, a);
     else
-        hipLaunchKernelGGL((render_bwd_mfma_kernel<SMAX>), dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0,
-                           stream, a);
+        hipLaunchKernelGGL((render_bwd_mfma_kernel<SMAX, false>), dim3(grid), dim3(kBlock), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -424,10 +424,12 @@ def test_backward_mfma_matches_dpp_variant(hip_ext, S):
     h = hip_forward(hip_ext, scene, cam, S=S)
     dc, do, dd, df = upstream_grads(cam.height, cam.width, S)
     gm = hip_backward(hip_ext, h, dc, do, dd, df)
-    os.environ["R3DG_BWD"] = "dpp"
-    try:
-        gd = hip_backward(hip_ext, h, dc, do, dd, df)
-    finally:
-        del os.environ["R3DG_BWD"]
-    for k in gm:
-        assert_close(k, gm[k], gd[k], 1e-5 * max(float(np.abs(gd[k]).max()) if gd[k].size else 0.0, 1e-12), 1e-3)
+    for variant in ("dpp", "wave"):  # DPP reductions; one-wave-per-quadrant workgroups
+        os.environ["R3DG_BWD"] = variant
+        try:
+            gd = hip_backward(hip_ext, h, dc, do, dd, df)
+        finally:
+            del os.environ["R3DG_BWD"]
+        for k in gm:
+            assert_close(f"{variant} {k}", gm[k], gd[k],
+                         1e-5 * max(float(np.abs(gd[k]).max()) if gd[k].size else 0.0, 1e-12), 1e-3)

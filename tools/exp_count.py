@@ -14,7 +14,9 @@ lib = ctypes.CDLL(os.path.join(r3.LIB_DIR, "libr3dg_hip.so"))
 buf, fb = (ctypes.c_ulonglong * 8)(), (ctypes.c_ulonglong * 8)()
 lib.r3dg_exp_counters_bwd(buf)
 lib.r3dg_exp_counters_fwd(fb)
-buf[2], buf[3] = fb[2], fb[3]
-names = ["bwd live pairs", "bwd mfma groups", "fwd steps done", "fwd live pairs (pre-exit)"]
+names = ["bwd live pairs", "bwd mfma groups", "bwd staging wall ticks (sum over waves)",
+         "bwd batch-loop wall ticks (sum over waves)"]
 for i, n in enumerate(names):
     print(f"{n}: {buf[i]}")
+print(f"bwd staging fraction: {buf[2] / max(buf[3], 1):.3f}")
+print(f"fwd steps done: {fb[2]}\nfwd live pairs (pre-exit): {fb[3]}")
