@@ -69,11 +69,14 @@ render_fwd_kernel(RenderFwdArgs a) {
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) F[c] = 0.f;
 
+    // Gaussian ids loaded one batch ahead: staging waits for one dependent round trip, not two
+    uint32_t gid_next = (t < NB && t < n) ? a.point_list[range.x + t] : 0u;
     for (int base = 0; base < n; base += NB) {
         if (__syncthreads_count(done) == kBlock) break;
         uint32_t m = 0;
         if (t < NB && base + t < n) {
-            const uint32_t gid = a.point_list[range.x + base + t];
+            const uint32_t gid = gid_next;
+            gid_next = (base + NB + t < n) ? a.point_list[range.x + base + NB + t] : 0u;
             if constexpr (!SHADER) {
                 // one contiguous render record per Gaussian (r3dg_kernels.h record_f4)
                 const float4* rec = a.records + (size_t)gid * (2 + NA4);
