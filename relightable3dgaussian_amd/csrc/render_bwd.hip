@@ -228,6 +228,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef R3DG_BWD_NB
 #define R3DG_BWD_NB 64  // instances staged per batch
 #endif
+#ifndef R3DG_BWD_PF
+#define R3DG_BWD_PF 0  // 1: conic / position of the next instance pair read one iteration ahead
+#endif
 #ifndef R3DG_BWD_PKDOT
 #define R3DG_BWD_PKDOT 1  // the per-pixel channel dot as packed fp32 FMAs
 #endif
@@ -363,12 +366,10 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     // One blend step of the reference's per-pixel loop (backward.cu:520-611), predicated rather
     // than branched: every LDS read is issued up front and a non-contributing pixel (outside,
     // past n_contrib, power > 0 or alpha < 1/255) leaves its state unchanged.
-    auto step = [&](int j, int p, bool live, float& wv, float& qv) {
+    auto step = [&](int j, int p, bool live, float4 co, float2 xy, float& wv, float& qv) {
 #pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
         const int ju = __builtin_amdgcn_readfirstlane(j);  // uniform addresses
         const float4* rj = s_rec + ju * SF4;
-        const float4 co = rj[0];
-        const float2 xy = s_xy[ju];
         float v[NA4 * 4];
 #pragma unroll
         for (int q = 0; q < NA4; ++q) {
@@ -514,17 +515,50 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             if (lo >= 32) bits = 0;
             else if (lo > 0) bits &= ~0u << lo;
             if (l == 0) R3DG_EXP_ADD(0, __builtin_popcount(bits));
-            while (bits) {
-                // two compacted instances per iteration: the second one's LDS reads and exp
-                // overlap the first one's dependent chain
-                const int j0 = c * 32 + __builtin_ctz(bits);
+            // two compacted instances per iteration: the second one's LDS reads and exp overlap
+            // the first one's dependent chain. R3DG_BWD_PF: the next pair's conic and position
+            // are read one iteration ahead, so a pair's chain does not start with an LDS wait.
+            auto take = [&](int& ja, int& jb, bool& hb) {
+                ja = c * 32 + __builtin_ctz(bits);
                 bits &= bits - 1;
-                const bool has1 = bits != 0u;
-                const int j1 = has1 ? c * 32 + __builtin_ctz(bits) : j0;
+                hb = bits != 0u;
+                jb = hb ? c * 32 + __builtin_ctz(bits) : ja;
                 bits &= bits - 1;
+            };
+            auto rec0 = [&](int j) { return s_rec[__builtin_amdgcn_readfirstlane(j) * SF4]; };
+            auto pos = [&](int j) { return s_xy[__builtin_amdgcn_readfirstlane(j)]; };
+#if R3DG_BWD_PF
+            int j0 = 0, j1 = 0;
+            bool has1 = false;
+            float4 co0 = make_float4(0.f, 0.f, 0.f, 0.f), co1 = co0;
+            float2 xy0 = make_float2(0.f, 0.f), xy1 = xy0;
+            bool cur = bits != 0u;
+            if (cur) {
+                take(j0, j1, has1);
+                co0 = rec0(j0); co1 = rec0(j1); xy0 = pos(j0); xy1 = pos(j1);
+            }
+            while (cur) {
+                int n0 = 0, n1 = 0;
+                bool nh1 = false;
+                float4 nco0 = co0, nco1 = co1;
+                float2 nxy0 = xy0, nxy1 = xy1;
+                const bool nxt = bits != 0u;
+                if (nxt) {
+                    take(n0, n1, nh1);
+                    nco0 = rec0(n0); nco1 = rec0(n1); nxy0 = pos(n0); nxy1 = pos(n1);
+                }
                 float wv0, qv0, wv1, qv1;
-                step(j0, hi - 1 - j0, true, wv0, qv0);
-                step(j1, hi - 1 - j1, has1, wv1, qv1);
+                step(j0, hi - 1 - j0, true, co0, xy0, wv0, qv0);
+                step(j1, hi - 1 - j1, has1, co1, xy1, wv1, qv1);
+#else
+            while (bits) {
+                int j0, j1;
+                bool has1;
+                take(j0, j1, has1);
+                float wv0, qv0, wv1, qv1;
+                step(j0, hi - 1 - j0, true, rec0(j0), pos(j0), wv0, qv0);
+                step(j1, hi - 1 - j1, has1, rec0(j1), pos(j1), wv1, qv1);
+#endif
                 float* wr = wq + r * WQS + l;
                 wr[0] = wv0;
                 wr[GRP * WQS] = qv0;
@@ -539,6 +573,11 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
                     flush(r);
                     r = 0;
                 }
+#if R3DG_BWD_PF
+                cur = nxt;
+                j0 = n0; j1 = n1; has1 = nh1;
+                co0 = nco0; co1 = nco1; xy0 = nxy0; xy1 = nxy1;
+#endif
             }
         }
     }
