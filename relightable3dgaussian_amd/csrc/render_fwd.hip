@@ -34,6 +34,9 @@ R3DG_EXP_READER(r3dg_exp_counters_fwd)
 #ifndef R3DG_FWD_PRED
 #define R3DG_FWD_PRED 0  // 1: accumulation predicated (weight 0) instead of branched (measured slower)
 #endif
+#ifndef R3DG_FWD_HOIST
+#define R3DG_FWD_HOIST 0  // 1: both paired instances' conic / position read up front (measured: no gain)
+#endif
 #ifndef R3DG_FWD_PAIR
 #define R3DG_FWD_PAIR 1  // two compacted instances per loop iteration
 #endif
@@ -126,10 +129,8 @@ render_fwd_kernel(RenderFwdArgs a) {
         __syncthreads();
         // One blend step of renderCUDA (forward.cu:470-520): the tests are predicated, every LDS
         // read of the instance is issued before them, and only the accumulation is a branch.
-        auto step = [&](int j, bool live) {
+        auto step = [&](int j, bool live, float4 co, float2 xy) {
 #pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
-            const float2 xy = s_xy[j];
-            const float4 co = s_co[j];
             float v[NA4 * 4];
 #pragma unroll
             for (int q = 0; q < NA4; ++q) {
@@ -197,13 +198,22 @@ render_fwd_kernel(RenderFwdArgs a) {
                 const bool has1 = bits != 0u;
                 const int j1 = has1 ? c * 32 + __builtin_ctz(bits) : j0;
                 bits &= bits - 1;
-                step(j0, true);
-                step(j1, has1);
+#if R3DG_FWD_HOIST
+                // both instances' conic / position read before the first step's tests: the second
+                // step's reads no longer wait behind the first step's accumulation branch
+                const float4 co0 = s_co[j0], co1 = s_co[j1];
+                const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
+                step(j0, true, co0, xy0);
+                step(j1, has1, co1, xy1);
+#else
+                step(j0, true, s_co[j0], s_xy[j0]);
+                step(j1, has1, s_co[j1], s_xy[j1]);
+#endif
                 if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
 #else
                 const int j0 = c * 32 + __builtin_ctz(bits);
                 bits &= bits - 1;
-                step(j0, true);
+                step(j0, true, s_co[j0], s_xy[j0]);
 #endif
                 if (__ballot(!done) == 0ull) {  // converged here: a uniform exit
                     alive = false;
