@@ -151,6 +151,15 @@ typedef struct r3dg_backward_outputs {
     float* dL_dsh;        /* [P,M,3] (may be NULL when M == 0) */
     float* dL_dscales;    /* [P,3] */
     float* dL_drotations; /* [P,4] */
+    /* Optional chunked delivery (zero-initialised: one chunk, no callback). The per-Gaussian phase
+     * (partial-row sums, cov2D / projection / SH / cov3D backward) runs over n_chunks contiguous
+     * Gaussian ranges, 256-aligned, in order; after the kernels of [g_begin, g_end) are enqueued
+     * on the stream, chunk_done(chunk_ctx, chunk, g_begin, g_end) is called on the host, so the
+     * caller can start exchanging that range's gradients (an RCCL all-reduce on another stream)
+     * while the next range computes. Results do not depend on n_chunks. */
+    int n_chunks;
+    void (*chunk_done)(void* ctx, int chunk, int g_begin, int g_end);
+    void* chunk_ctx;
 } r3dg_backward_outputs;
 
 /* RasterizeGaussiansBackwardCUDA (rasterize_points.cu:183-275). Every output element is written

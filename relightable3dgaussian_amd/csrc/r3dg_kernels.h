@@ -99,6 +99,7 @@ struct RenderBwdArgs {
 
 struct GatherBwdArgs {
     int P, D, M, S, RS, W, H, grid_x, grid_y;
+    int g_begin, g_end;       // Gaussian range of this launch (outputs indexed by global id)
     const float* rows;        // partial rows (RenderBwdArgs)
     const float* zero_row;    // RS zeros: the load target of quadrants without a row
     float* sums;              // [P, RS] per-Gaussian sums (row_sum_kernel -> gather_bwd_kernel)

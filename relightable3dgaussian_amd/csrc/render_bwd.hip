@@ -861,14 +861,14 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
     constexpr int CH = 8;                         // slots per chunk (one flag word per lane)
     const int RS = a.RS;
     const int t = blockIdx.x * 256 + threadIdx.x;
-    const int g = t / LPG, c = t % LPG;
-    const bool active = g < a.P && c < NXC + 2;
+    const int g = a.g_begin + t / LPG, c = t % LPG;
+    const bool active = g < a.g_end && c < NXC + 2;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     float S0 = 0.f, Sdx = 0.f, Sdy = 0.f, Sdxdx = 0.f, Sdxdy = 0.f, Sdydy = 0.f;
     uint32_t k0 = 0, n = 0;
     float2 xy = make_float2(0.f, 0.f);
     int x0 = 0, y0 = 0, rw = 1;
-    if (g < a.P && a.rows && a.radii[g] > 0) {  // uniform within the group
+    if (g < a.g_end && a.rows && a.radii[g] > 0) {  // uniform within the group
         k0 = g == 0 ? 0u : a.offsets[g - 1];
         n = a.offsets[g] - k0;
         xy = a.means2D[g];
@@ -948,13 +948,13 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     constexpr int SHS = 49;                // LDS stride of one Gaussian's SH block (<= 48 used, odd)
     __shared__ float s_buf[256 * SHS];
     const int t = threadIdx.x;
-    const int g0 = blockIdx.x * 256;
+    const int g0 = a.g_begin + blockIdx.x * 256;
     const int g = g0 + t;
     const int S = a.S;
 
     // sum row -> the kRow layout gather_gaussian reads
     float s[NR];
-    if (g < a.P) {
+    if (g < a.g_end) {
         const float4* src = reinterpret_cast<const float4*>(a.sums + (size_t)g * a.RS);
         float x[XW + 8];
 #pragma unroll
@@ -980,7 +980,7 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     }
     // ---- SH coefficients of the block's Gaussians: one coalesced copy into LDS ----
     const int M3 = 3 * a.M;
-    const int ng = min(256, a.P - g0);
+    const int ng = min(256, a.g_end - g0);
     float* shl = s_buf + t * SHS;
     if (a.sh && a.dL_dsh) {
         const float* src = a.sh + (size_t)g0 * M3;
@@ -990,7 +990,7 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
         }
     }
     __syncthreads();
-    if (g < a.P) gather_gaussian<SMAX>(a, g, s, shl);
+    if (g < a.g_end) gather_gaussian<SMAX>(a, g, s, shl);
     __syncthreads();
     if (a.dL_dsh) {
         float* dst = a.dL_dsh + (size_t)g0 * M3;
@@ -1005,9 +1005,11 @@ template <int SMAX>
 static hipError_t launch_gather_s(const GatherBwdArgs& a, hipStream_t stream) {
     constexpr int NXC = 4 * ((4 + SMAX + 15) / 16);
     constexpr int LPG = NXC + 2 <= 8 ? 8 : 16;
-    const long long threads = (long long)a.P * LPG;
+    const int n = a.g_end - a.g_begin;
+    if (n <= 0) return hipSuccess;
+    const long long threads = (long long)n * LPG;
     hipLaunchKernelGGL((row_sum_kernel<SMAX>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL((gather_bwd_kernel<SMAX>), dim3((a.P + 255) / 256), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((gather_bwd_kernel<SMAX>), dim3((n + 255) / 256), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

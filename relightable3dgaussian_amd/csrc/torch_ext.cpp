@@ -147,7 +147,8 @@ BwdResult backward_impl(const torch::Tensor& background, const torch::Tensor& me
                         const torch::Tensor& sh, int64_t degree, const torch::Tensor& campos,
                         const torch::Tensor& geomBuffer, int64_t R, const torch::Tensor& binningBuffer,
                         const torch::Tensor& imageBuffer, bool backward_geometry, bool debug, int H, int W,
-                        bool color_hwc, bool feature_native) {
+                        bool color_hwc, bool feature_native, int n_chunks = 1,
+                        const py::object& chunk_cb = py::none()) {
     const torch::Device dev = means3D.device();
     const c10::OptionalDeviceGuard guard(dev);
     const int P = (int)means3D.size(0);
@@ -193,12 +194,36 @@ BwdResult backward_impl(const torch::Tensor& background, const torch::Tensor& me
     o.dL_dfeatures = S > 0 ? dL_dfeatures.data_ptr<float>() : nullptr; o.dL_dcov3D = dL_dcov3D.data_ptr<float>();
     o.dL_dsh = M > 0 ? dL_dsh.data_ptr<float>() : nullptr; o.dL_dscales = dL_dscales.data_ptr<float>();
     o.dL_drotations = dL_drotations.data_ptr<float>();
+    // chunked delivery: the Python callable runs (GIL held: we are inside the pybind call) after
+    // each Gaussian range's kernels are enqueued; an exception is re-raised after the C call
+    struct ChunkCtx {
+        const py::object* cb;
+        py::tuple outs;  // the 9 output tensors, handed to the callback
+        bool failed = false;
+        std::string what;
+    } cctx{&chunk_cb, py::make_tuple(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dfeatures, dL_dcov3D,
+                                     dL_dsh, dL_dscales, dL_drotations)};
+    o.n_chunks = n_chunks;
+    if (!chunk_cb.is_none()) {
+        o.chunk_ctx = &cctx;
+        o.chunk_done = [](void* ctx, int c, int g0, int g1) {
+            auto* k = static_cast<ChunkCtx*>(ctx);
+            if (k->failed) return;
+            try {
+                (*k->cb)(c, g0, g1, k->outs);
+            } catch (const std::exception& e) {
+                k->failed = true;
+                k->what = e.what();
+            }
+        };
+    }
     auto bopt = torch::TensorOptions().dtype(torch::kUInt8).device(dev);
     TensorAlloc scratch{bopt, torch::empty({0}, bopt)};
     check(r3dg_rasterize_gaussians_backward(&s, &g, rad.data_ptr<int>(), &gr, geomBuffer.data_ptr(),
                                             binningBuffer.data_ptr(), imageBuffer.data_ptr(), (int)R,
                                             backward_geometry, tensor_alloc, &scratch, &o, stream_of(dev)),
           "rasterize_gaussians_backward");
+    TORCH_CHECK(!cctx.failed, "rasterize_gaussians_backward: chunk callback raised: ", cctx.what);
     return {dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dfeatures, dL_dcov3D, dL_dsh, dL_dscales,
             dL_drotations};
 }
@@ -240,6 +265,26 @@ BwdResult rasterize_gaussians_backward_ex(const torch::Tensor& background, const
                          cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_opacity,
                          dL_dout_depth, dL_dout_feature, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
                          backward_geometry, debug, (int)H, (int)W, true, true);
+}
+
+// rasterize_gaussians_backward_ex with chunked delivery (include/r3dg_hip.h r3dg_backward_outputs):
+// chunk_cb(chunk, g_begin, g_end, outputs) is called once the gradients of Gaussians [g_begin,
+// g_end) are enqueued (outputs = the 9 result tensors), e.g. to start their all-reduce on a
+// communication stream (view_parallel.py).
+BwdResult rasterize_gaussians_backward_chunked(
+    const torch::Tensor& background, const torch::Tensor& means3D, const torch::Tensor& features,
+    const torch::Tensor& radii, const torch::Tensor& colors, const torch::Tensor& scales,
+    const torch::Tensor& rotations, double scale_modifier, const torch::Tensor& cov3D_precomp,
+    const torch::Tensor& viewmatrix, const torch::Tensor& projmatrix, double tan_fovx, double tan_fovy,
+    const torch::Tensor& dL_dout_color, const torch::Tensor& dL_dout_opacity, const torch::Tensor& dL_dout_depth,
+    const torch::Tensor& dL_dout_feature, const torch::Tensor& sh, int64_t degree, const torch::Tensor& campos,
+    const torch::Tensor& geomBuffer, int64_t R, const torch::Tensor& binningBuffer, const torch::Tensor& imageBuffer,
+    bool backward_geometry, bool debug, int64_t H, int64_t W, bool color_hwc, bool feature_native, int64_t n_chunks,
+    const py::object& chunk_cb) {
+    return backward_impl(background, means3D, features, radii, colors, scales, rotations, scale_modifier,
+                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_opacity,
+                         dL_dout_depth, dL_dout_feature, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                         backward_geometry, debug, (int)H, (int)W, color_hwc, feature_native, (int)n_chunks, chunk_cb);
 }
 
 torch::Tensor mark_visible(torch::Tensor& means3D, torch::Tensor& viewmatrix, torch::Tensor& projmatrix) {
@@ -638,6 +683,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("UploadTexturesToDevice", &upload_textures);
     // extensions
     m.def("rasterize_gaussians_backward_ex", &rasterize_gaussians_backward_ex);
+    m.def("rasterize_gaussians_backward_chunked", &rasterize_gaussians_backward_chunked);
     m.def("render_equation_forward_with_rand", &render_equation_forward_with_rand);
     m.def("rasterizer_state", &rasterizer_state);
     m.def("feature_groups", &feature_groups);

@@ -51,6 +51,51 @@ def all_reduce_grads(grads, group=None) -> dict:
     return unflatten_grads(flat, grads)
 
 
+_COMM = {}
+
+
+def chunk_all_reduce_hook(works: list, group=None, stream=None):
+    """Chunk callback for `_C.rasterize_gaussians_backward_chunked`: all-reduces the exchanged
+    gradient slices of Gaussians [g0, g1) (rows of contiguous [P, ...] tensors, so each slice is
+    contiguous) on a communication stream that first waits for the chunk's kernels, while the
+    compute stream goes on with the next chunk. `works` collects the async handles."""
+    import torch
+    import torch.distributed as dist
+
+    def hook(chunk, g0, g1, outs):
+        cur = torch.cuda.current_stream()
+        comm = stream
+        if comm is None:
+            comm = _COMM.setdefault(cur.device, torch.cuda.Stream(device=cur.device))
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        comm.wait_event(ev)
+        with torch.cuda.stream(comm):
+            for _, i in GRAD_FIELDS:
+                t = outs[i]
+                if t.numel():
+                    works.append(dist.all_reduce(t[g0:g1], group=group, async_op=True))
+
+    return hook
+
+
+def backward_all_reduce(_C, bwd_args, n_chunks: int = 4, group=None):
+    """rasterize_gaussians_backward_chunked(*bwd_args, n_chunks, hook) with the exchanged fields
+    summed over ranks chunk by chunk, overlapped with the remaining per-Gaussian kernels (the
+    blend must finish before any Gaussian's gradient is final, so only that phase overlaps).
+    `bwd_args` is the rasterize_gaussians_backward_ex argument list + (color_hwc, feature_native).
+    Returns the backward 9-tuple; the current stream waits for the exchange."""
+    import torch.distributed as dist
+
+    works = []
+    multi = dist.is_initialized() and dist.get_world_size(group) > 1
+    hook = chunk_all_reduce_hook(works, group) if multi else None
+    grads = _C.rasterize_gaussians_backward_chunked(*bwd_args, n_chunks if multi else 1, hook)
+    for w in works:
+        w.wait()
+    return grads
+
+
 def rank_yaw(rank: int, world: int, step_deg: float = 1.0) -> np.ndarray:
     """Rotation of rank `rank`'s camera: a small yaw so every view costs about the same."""
     if world == 1:

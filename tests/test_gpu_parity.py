@@ -14,7 +14,7 @@ import pytest
 
 import oracle
 from relightable3dgaussian_amd import synthetic
-from tests._helpers import assert_close, hip_backward, hip_forward, upstream_grads
+from tests._helpers import assert_close, hip_backward, hip_forward, tt, upstream_grads
 
 pytestmark = pytest.mark.gpu
 
@@ -433,3 +433,82 @@ def test_backward_mfma_matches_dpp_variant(hip_ext, S):
         for k in gm:
             assert_close(f"{variant} {k}", gm[k], gd[k],
                          1e-5 * max(float(np.abs(gd[k]).max()) if gd[k].size else 0.0, 1e-12), 1e-3)
+
+
+def test_backward_chunked_delivery(hip_ext):
+    """Chunked per-Gaussian phase (r3dg_backward_outputs.n_chunks / chunk_done): bitwise the same
+    gradients as one chunk; the callback sees 256-aligned ranges covering every Gaussian in order,
+    with the output tensors (view_parallel.backward_all_reduce overlaps the exchange with it)."""
+    scene, cam = synthetic.small_scene(P=3000, S=11, seed=77, width=96, height=80)
+    h = hip_forward(hip_ext, scene, cam, S=11)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11)
+    ref = hip_backward(hip_ext, h, dc, do, dd, df)
+    a = h["_args"]
+    seen = []
+
+    def hook(c, g0, g1, outs):
+        seen.append((c, g0, g1, len(outs)))
+
+    args = (tt(h["_bg"]), a["means3D"], a["features"], h["radii"], a["colors"], a["scales"], a["rotations"], 1.0,
+            a["cov3D"], tt(cam.view), tt(cam.proj), cam.tanfovx, cam.tanfovy, tt(dc), tt(do), tt(dd), tt(df), a["sh"],
+            3, tt(cam.campos), h["geom"], h["num_rendered"], h["binning"], h["image"], True, False, cam.height,
+            cam.width, False, False)
+    out = hip_ext.rasterize_gaussians_backward_chunked(*args, 5, hook)
+    P = scene.P
+    assert [s[0] for s in seen] == list(range(len(seen))) and len(seen) > 1
+    assert seen[0][1] == 0 and seen[-1][2] == P and all(s[3] == 9 for s in seen)
+    assert all(a[2] == b[1] for a, b in zip(seen, seen[1:])) and all(s[1] % 256 == 0 for s in seen)
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dfeatures", "dL_dcov3D", "dL_dsh",
+             "dL_dscales", "dL_drotations"]
+    for i, k in enumerate(names):
+        np.testing.assert_array_equal(out[i].cpu().numpy().reshape(ref[k].shape), ref[k], err_msg=k)
+
+
+def _chunked_exchange_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    import relightable3dgaussian_amd as r3
+    from relightable3dgaussian_amd import view_parallel
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    scene, cam = synthetic.small_scene(P=2500, S=11, seed=91, width=96, height=80)
+    h = hip_forward(r3._C, scene, cam, S=11)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11)
+    local = hip_backward(r3._C, h, dc, do, dd, df)
+    a = h["_args"]
+    args = (tt(h["_bg"]), a["means3D"], a["features"], h["radii"], a["colors"], a["scales"], a["rotations"], 1.0,
+            a["cov3D"], tt(cam.view), tt(cam.proj), cam.tanfovx, cam.tanfovy, tt(dc), tt(do), tt(dd), tt(df), a["sh"],
+            3, tt(cam.campos), h["geom"], h["num_rendered"], h["binning"], h["image"], True, False, cam.height,
+            cam.width, False, False)
+    out = view_parallel.backward_all_reduce(r3._C, args, n_chunks=4)
+    torch.cuda.synchronize()
+    res = {name: out[i].cpu().numpy() for name, i in view_parallel.GRAD_FIELDS}
+    q.put((rank, res, {"means3D": local["dL_dmeans3D"], "sh": local["dL_dsh"], "opacity": local["dL_dopacity"],
+                       "scales": local["dL_dscales"], "rotations": local["dL_drotations"],
+                       "features": local["dL_dfeatures"]}))
+    dist.destroy_process_group()
+
+
+def test_view_parallel_chunked_exchange_two_ranks(hip_ext):
+    """bench.py's N > 1 path on one GPU: two gloo ranks render the same view, the chunked
+    all-reduce (overlapped with the gather phase) must return exactly 2x the local gradients."""
+    import multiprocessing as mp
+    import socket
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_chunked_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, res, local in got:
+        for k, v in res.items():
+            np.testing.assert_array_equal(v.reshape(local[k].shape), 2 * local[k], err_msg=f"rank {rank} {k}")
