@@ -54,9 +54,9 @@ def _check_forward(h, o, S):
     np.testing.assert_array_equal(h["stencil"].cpu().numpy(), 0.0)
 
 
-@pytest.mark.parametrize("S", [0, 3, 11, 21])
+@pytest.mark.parametrize("S", [0, 3, 11, 21, 32])
 def test_forward_matches_oracle(hip_ext, S):
-    scene, cam = synthetic.small_scene(P=3000, S=21, seed=S, width=96, height=72)
+    scene, cam = synthetic.small_scene(P=3000, S=max(S, 21), seed=S, width=96, height=72)
     h = hip_forward(hip_ext, scene, cam, S=S)
     o = _oracle_fwd(scene, cam, S)
     _check_forward(h, o, S)
@@ -102,9 +102,9 @@ def _grad_tol(ref):
     return 2e-5 * max(float(np.abs(ref).max()) if ref.size else 0.0, 1e-12)
 
 
-@pytest.mark.parametrize("S", [0, 11, 21])
+@pytest.mark.parametrize("S", [0, 11, 21, 24, 32])
 def test_backward_matches_oracle(hip_ext, S):
-    scene, cam = synthetic.small_scene(P=2500, S=21, seed=10 + S, width=96, height=64)
+    scene, cam = synthetic.small_scene(P=2500, S=max(S, 21), seed=10 + S, width=96, height=64)
     h = hip_forward(hip_ext, scene, cam, S=S)
     o = _oracle_fwd(scene, cam, S)
     dc, do, dd, df = upstream_grads(cam.height, cam.width, S)
