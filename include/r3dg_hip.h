@@ -338,6 +338,45 @@ int r3dg_densify_and_prune(const r3dg_param_layout* layout, const float* param, 
 int r3dg_reset_opacity(const r3dg_param_layout* layout, float* param, float* exp_avg, float* exp_avg_sq,
                        r3dg_stream_t stream);
 
+/* ---- BVH visibility tracer (reference module bvh_tracing._C,
+ *      bvh/src/bindings.cpp:9-11) ------------------------------------------------------------
+ * Tree layout (the reference's, bvh/__init__.py:31-37): nodes int32 [2P-1, 5] rows
+ * {parent, left, right, gaussian, leaf count}, internal nodes 0..P-2, leaf P-1+i holds the i-th
+ * Gaussian in Morton order; aabbs f32 [2P-1, 6] rows {lower xyz, upper xyz}; morton u64 [P]
+ * sorted keys (30-bit Morton code << 31 | Gaussian index). */
+
+/* RayTracer.__init__ leaf boxes (bvh/__init__.py:29-59): per Gaussian the min / max of the 8
+ * corners mean ± 3 s_k R[:, k] (R = build_rotation of the re-normalised quaternion, r x y z),
+ * written as [P, 6] rows to leaf_aabbs (pass aabbs + 6 (P - 1) to fill the tree's leaf rows). */
+int r3dg_bvh_leaf_aabbs(int P, const float* means3D, const float* scales, const float* rotations,
+                        float* leaf_aabbs, r3dg_stream_t stream);
+
+/* create_bvh (bvh/src/bvh.cu:8-26, construct.cu:148-265): Karras LBVH over the leaf boxes in
+ * aabbs rows P-1..2P-2 (input, in Gaussian order). Writes every field of nodes, the internal and
+ * (Morton-sorted) leaf rows of aabbs, and morton. P >= 1. Scratch from scratch_alloc. */
+int r3dg_bvh_build(int P, int32_t* nodes, float* aabbs, uint64_t* morton, r3dg_alloc_fn scratch_alloc,
+                   void* scratch_ctx, r3dg_stream_t stream);
+
+/* trace_bvh_opacity (bvh/src/bvh.cu:87-117, trace.cu:199-286): per ray the transmittance through
+ * the Gaussians it meets (cov3D_inv: [P, 6] upper-triangular inverse covariance, the
+ * get_inverse_covariance of gaussian_model.py:410-413). Outputs: num_contributes int32 [R],
+ * rendered_opacity f32 [R] (0 and 0 once the transmittance drops below 0.9). num_gaussians = P of
+ * the tree (2P-1 nodes); it bounds the traversal, so a malformed tree cannot hang the GPU. */
+int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int32_t* nodes, const float* aabbs, const float* rays_o,
+                           const float* rays_d, const float* means3D, const float* cov3D_inv,
+                           const float* opacities, const float* normals, int32_t* num_contributes,
+                           float* rendered_opacity, r3dg_stream_t stream);
+
+/* trace_bvh (bvh/src/bvh.cu:28-85, trace.cu:8-196): per ray the Gaussians of every crossed
+ * subtree of <= 4 leaves, sorted by (ray, t); num_contributes int32 [R] is their count per ray.
+ * The three lists (int32 [L], f32 [L, 3], int32 [L]) come from alloc; *num_rendered = L (one
+ * blocking device-to-host copy, as the reference). The reference's covs3D / opacities arguments
+ * do not enter its arithmetic and are not taken here. */
+int r3dg_bvh_trace(int num_rays, int num_gaussians, const int32_t* nodes, const float* aabbs, const float* rays_o,
+                   const float* rays_d, const float* means3D, int32_t* num_contributes, r3dg_alloc_fn alloc,
+                   void* alloc_ctx, int* num_rendered, int32_t** point_list, float** position_list,
+                   int32_t** ray_id_list, r3dg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

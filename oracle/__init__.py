@@ -24,7 +24,7 @@ F = np.float32
 
 
 def build() -> str:
-    srcs = [os.path.join(HERE, f) for f in ("r3dg_oracle.c", "r3dg_shaders.c", "Makefile")]
+    srcs = [os.path.join(HERE, f) for f in ("r3dg_oracle.c", "r3dg_shaders.c", "r3dg_bvh.c", "Makefile")]
     if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return _LIB
@@ -413,3 +413,56 @@ def brdf_backward(inp, incident_dirs, dL_dpbr, dL_ddiffuse, sample_num=24):
         _p(o["rough"]), _p(o["metal"]), _p(o["normals"]), _p(o["viewdirs"]), _p(o["incidents"]), _p(o["env"]),
         _p(o["visibility"]))
     return o
+
+
+# ---- BVH visibility tracer (r3dg_bvh.c; reference bvh/src/*.cu, bvh/__init__.py) -------------
+
+def bvh_leaf_aabbs(means3D, scales, rotations):
+    m, s, r = _f(means3D), _f(scales), _f(rotations)
+    P = m.shape[0]
+    out = np.zeros((P, 6), F)
+    lib().oracle_bvh_leaf_aabbs(ctypes.c_int(P), _p(m), _p(s), _p(r), _p(out))
+    return out
+
+
+def bvh_build(leaf_aabbs):
+    """create_bvh on leaf boxes in Gaussian order -> (nodes int32 [2P-1,5], aabbs [2P-1,6], morton u64 [P])."""
+    leaf = _f(leaf_aabbs)
+    P = leaf.shape[0]
+    nodes = np.full((2 * P - 1, 5), -1, np.int32)
+    aabbs = np.zeros((2 * P - 1, 6), F)
+    aabbs[P - 1:] = leaf
+    keys = np.zeros(P, np.uint64)
+    rc = lib().oracle_bvh_build(ctypes.c_int(P), _p(nodes), _p(aabbs), _p(keys))
+    assert rc == 0, "oracle_bvh_build failed"
+    return nodes, aabbs, keys
+
+
+def bvh_trace_opacity(nodes, aabbs, rays_o, rays_d, means3D, cov_inv, opacity, normals):
+    """trace_bvh_opacity -> (contribute int32 [R], visibility f32 [R], transmittance before the cut [R])."""
+    o, d = _f(rays_o).reshape(-1, 3), _f(rays_d).reshape(-1, 3)
+    R = o.shape[0]
+    contrib = np.zeros(R, np.int32)
+    vis = np.ones(R, F)
+    t_last = np.ones(R, F)
+    lib().oracle_bvh_trace_opacity(ctypes.c_int(R), _p(np.ascontiguousarray(nodes, np.int32)), _p(_f(aabbs)), _p(o),
+                                   _p(d), _p(_f(means3D)), _p(_f(cov_inv)), _p(_f(opacity).reshape(-1)),
+                                   _p(_f(normals)), _p(contrib), _p(vis), _p(t_last))
+    return contrib, vis, t_last
+
+
+def bvh_trace(nodes, aabbs, rays_o, rays_d, means3D):
+    """trace_bvh -> (contribute int32 [R], point [L], position [L,3], ray_id [L])."""
+    nd, bx, o, d, m = (np.ascontiguousarray(nodes, np.int32), _f(aabbs), _f(rays_o).reshape(-1, 3),
+                       _f(rays_d).reshape(-1, 3), _f(means3D))
+    R = o.shape[0]
+    contrib = np.zeros(R, np.int32)
+    lib().oracle_bvh_trace.restype = ctypes.c_long
+    L = lib().oracle_bvh_trace(ctypes.c_int(R), _p(nd), _p(bx), _p(o), _p(d), _p(m), _p(contrib), None, None, None)
+    point = np.zeros(max(L, 1), np.int32)
+    pos = np.zeros((max(L, 1), 3), F)
+    rid = np.zeros(max(L, 1), np.int32)
+    L2 = lib().oracle_bvh_trace(ctypes.c_int(R), _p(nd), _p(bx), _p(o), _p(d), _p(m), _p(contrib), _p(point),
+                                _p(pos), _p(rid))
+    assert L2 == L
+    return contrib, point[:L], pos[:L], rid[:L]

@@ -7,7 +7,8 @@ requires GPU tensors.
 
 `install_alias()` registers this package as `r3dg_rasterization` so the reference's
 `from r3dg_rasterization import _C` (gaussian_renderer/r3dg_rasterization.py:7-8,
-scene/gaussian_model.py:18) resolves here.
+scene/gaussian_model.py:18) resolves here, and `relightable3dgaussian_amd.bvh` as the reference's
+`bvh` package (`from bvh import RayTracer`, scene/gaussian_model.py:16) (INTEGRATION.md).
 """
 from __future__ import annotations
 
@@ -46,6 +47,10 @@ def install_alias() -> None:
 
     sys.modules.setdefault("r3dg_rasterization", wrapper)
     sys.modules.setdefault("r3dg_rasterization._C", _C)
+    # the reference's BVH tracer package (bvh/__init__.py) and its extension bvh_tracing._C
+    from .bvh import install_bvh_alias
+
+    install_bvh_alias()
 
 
 __all__ = ["_C", "install_alias", "HIP_LIB", "EXT_LIB"]

@@ -26,13 +26,13 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
 HIP_SOURCES = ["preprocess.hip", "render_fwd.hip", "render_bwd.hip", "brdf.hip", "shaders.hip", "rasterizer.hip",
-               "optim.hip"]
+               "optim.hip", "bvh.hip"]
 HIP_FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
              "-munsafe-fp-atomics", f"-I{INC}", f"-I{CSRC}"]
 # the key path (projection, radius, rect) must not contract a*b+c into fma: see preprocess.hip
 # render_bwd: the SLP vectorizer pairs the two unrolled blend steps into packed f32 ops plus
 # register shuffles (more instructions, 30 more VGPRs); plain scalar code measures faster
-PER_FILE_FLAGS = {"preprocess.hip": ["-ffp-contract=off"], "render_bwd.hip": ["-fno-slp-vectorize"]}
+PER_FILE_FLAGS = {"preprocess.hip": ["-ffp-contract=off"], "bvh.hip": ["-ffp-contract=off"], "render_bwd.hip": ["-fno-slp-vectorize"]}
 
 
 def _newer(target: str, deps: list[str]) -> bool:

@@ -662,6 +662,129 @@ void reset_opacity(int64_t P, const std::vector<int64_t>& widths, const std::vec
           "reset_opacity");
 }
 
+// ---- BVH visibility tracer: the reference's bvh_tracing._C (bvh/src/bindings.cpp:9-11) ----------
+
+torch::Tensor cuda_f32(const torch::Tensor& t, const char* what) {
+    TORCH_CHECK(t.is_cuda(), what, ": expected a GPU tensor (this build has no CPU path)");
+    TORCH_CHECK(t.scalar_type() == torch::kFloat32, what, ": expected float32");
+    return t.contiguous();
+}
+
+// RayTracer.__init__ leaf boxes (bvh/__init__.py:29-59) in one launch -> [P, 6]
+torch::Tensor bvh_leaf_aabbs(const torch::Tensor& means3D, const torch::Tensor& scales,
+                             const torch::Tensor& rotations) {
+    const auto m = cuda_f32(means3D, "bvh_leaf_aabbs"), s = cuda_f32(scales, "bvh_leaf_aabbs"),
+               r = cuda_f32(rotations, "bvh_leaf_aabbs");
+    const int64_t P = m.size(0);
+    TORCH_CHECK(m.numel() == 3 * P && s.numel() == 3 * P && r.numel() == 4 * P,
+                "bvh_leaf_aabbs: means3D [P,3], scales [P,3], rotations [P,4] expected");
+    const c10::OptionalDeviceGuard guard(m.device());
+    auto out = torch::empty({P, 6}, m.options());
+    check(r3dg_bvh_leaf_aabbs((int)P, m.data_ptr<float>(), s.data_ptr<float>(), r.data_ptr<float>(),
+                              out.data_ptr<float>(), stream_of(m.device())),
+          "bvh_leaf_aabbs");
+    return out;
+}
+
+// create_bvh (bvh/src/bvh.cu:8-26): fills nodes / aabbs in place (their leaf boxes are the input)
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> create_bvh(const torch::Tensor& means3D,
+                                                                   const torch::Tensor& scales,
+                                                                   const torch::Tensor& rotations,
+                                                                   torch::Tensor nodes, torch::Tensor aabbs) {
+    (void)scales;
+    (void)rotations;  // the reference takes them and does not read them (construct.cu:148-155)
+    const int64_t P = means3D.size(0);
+    TORCH_CHECK(nodes.is_cuda() && aabbs.is_cuda(), "create_bvh: expected GPU tensors");
+    TORCH_CHECK(nodes.scalar_type() == torch::kInt32 && aabbs.scalar_type() == torch::kFloat32,
+                "create_bvh: nodes int32, aabbs float32 expected");
+    TORCH_CHECK(nodes.is_contiguous() && aabbs.is_contiguous(), "create_bvh: nodes / aabbs must be contiguous");
+    TORCH_CHECK(P >= 1 && nodes.numel() == 5 * (2 * P - 1) && aabbs.numel() == 6 * (2 * P - 1),
+                "create_bvh: nodes [2P-1,5] and aabbs [2P-1,6] expected");
+    const c10::OptionalDeviceGuard guard(aabbs.device());
+    auto morton = torch::empty({P}, aabbs.options().dtype(torch::kInt64));
+    TensorAlloc scratch{aabbs.options().dtype(torch::kUInt8), {}};
+    check(r3dg_bvh_build((int)P, nodes.data_ptr<int32_t>(), aabbs.data_ptr<float>(),
+                         reinterpret_cast<uint64_t*>(morton.data_ptr<int64_t>()), tensor_alloc, &scratch,
+                         stream_of(aabbs.device())),
+          "create_bvh");
+    return {nodes, aabbs, morton};
+}
+
+// trace_bvh_opacity (bvh/src/bvh.cu:87-117): outputs shaped like rays_o without its last axis
+std::tuple<torch::Tensor, torch::Tensor> trace_bvh_opacity(const torch::Tensor& nodes, const torch::Tensor& aabbs,
+                                                           const torch::Tensor& rays_o, const torch::Tensor& rays_d,
+                                                           const torch::Tensor& means3D, const torch::Tensor& covs3D,
+                                                           const torch::Tensor& opacities,
+                                                           const torch::Tensor& normals) {
+    TORCH_CHECK(nodes.is_cuda() && nodes.scalar_type() == torch::kInt32, "trace_bvh_opacity: nodes int32 on GPU");
+    const auto o = cuda_f32(rays_o, "rays_o"), d = cuda_f32(rays_d, "rays_d");
+    TORCH_CHECK(o.dim() >= 1 && o.size(-1) == 3 && d.numel() == o.numel(), "trace_bvh_opacity: rays [..., 3]");
+    const int64_t R = o.numel() / 3;
+    const c10::OptionalDeviceGuard guard(o.device());
+    auto shape = o.sizes().slice(0, o.dim() - 1);
+    auto contrib = torch::zeros(shape, o.options().dtype(torch::kInt32));
+    auto vis = torch::ones(shape, o.options());
+    const auto nd = nodes.contiguous(), bx = cuda_f32(aabbs, "aabbs"), m = cuda_f32(means3D, "means3D"),
+               c = cuda_f32(covs3D, "covs3D"), op = cuda_f32(opacities, "opacities"), n = cuda_f32(normals, "normals");
+    const int64_t P = m.numel() / 3;
+    TORCH_CHECK(P >= 1 && nd.numel() == 5 * (2 * P - 1) && bx.numel() == 6 * (2 * P - 1) && c.numel() == 6 * P &&
+                    op.numel() == P && n.numel() == 3 * P,
+                "trace_bvh_opacity: tree / Gaussian shapes disagree");
+    check(r3dg_bvh_trace_opacity((int)R, (int)P, nd.data_ptr<int32_t>(), bx.data_ptr<float>(), o.data_ptr<float>(),
+                                 d.data_ptr<float>(), m.data_ptr<float>(), c.data_ptr<float>(), op.data_ptr<float>(),
+                                 n.data_ptr<float>(), contrib.data_ptr<int32_t>(), vis.data_ptr<float>(),
+                                 stream_of(o.device())),
+          "trace_bvh_opacity");
+    return {contrib, vis};
+}
+
+struct MultiAllocBvh {
+    torch::TensorOptions opts;
+    std::vector<torch::Tensor> ts;
+};
+void* multi_alloc_bvh(void* ctx, size_t n) {
+    auto* a = static_cast<MultiAllocBvh*>(ctx);
+    a->ts.push_back(torch::empty({(int64_t)std::max<size_t>(n, 256)}, a->opts));
+    return a->ts.back().data_ptr();
+}
+
+// trace_bvh (bvh/src/bvh.cu:28-85)
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor> trace_bvh(
+    const torch::Tensor& nodes, const torch::Tensor& aabbs, const torch::Tensor& rays_o, const torch::Tensor& rays_d,
+    const torch::Tensor& means3D, const torch::Tensor& covs3D, const torch::Tensor& opacities) {
+    (void)covs3D;
+    (void)opacities;  // unused by the reference's arithmetic (trace.cu:123-124 commented out)
+    TORCH_CHECK(nodes.is_cuda() && nodes.scalar_type() == torch::kInt32, "trace_bvh: nodes int32 on GPU");
+    const auto o = cuda_f32(rays_o, "rays_o"), d = cuda_f32(rays_d, "rays_d");
+    const int64_t R = o.size(0);
+    TORCH_CHECK(o.numel() == 3 * R && d.numel() == 3 * R, "trace_bvh: rays [R, 3]");
+    const c10::OptionalDeviceGuard guard(o.device());
+    const auto iopt = o.options().dtype(torch::kInt32);
+    auto contrib = torch::zeros({R, 1}, iopt);
+    const auto nd = nodes.contiguous(), bx = cuda_f32(aabbs, "aabbs"), m = cuda_f32(means3D, "means3D");
+    const int64_t P = m.numel() / 3;
+    TORCH_CHECK(P >= 1 && nd.numel() == 5 * (2 * P - 1) && bx.numel() == 6 * (2 * P - 1),
+                "trace_bvh: tree shapes disagree");
+    MultiAllocBvh al{o.options().dtype(torch::kUInt8), {}};
+    int L = 0;
+    int32_t *pt = nullptr, *rid = nullptr;
+    float* pos = nullptr;
+    check(r3dg_bvh_trace((int)R, (int)P, nd.data_ptr<int32_t>(), bx.data_ptr<float>(), o.data_ptr<float>(), d.data_ptr<float>(),
+                         m.data_ptr<float>(), contrib.data_ptr<int32_t>(), multi_alloc_bvh, &al, &L, &pt, &pos, &rid,
+                         stream_of(o.device())),
+          "trace_bvh");
+    if (L == 0)  // the reference's empty shapes (bvh.cu:48-53), ray_id_list float [0, 3] included
+        return {contrib, torch::zeros({0, 1}, iopt), torch::zeros({0, 3}, o.options()), torch::zeros({0, 3}, o.options())};
+    auto view = [&](void* p, std::vector<int64_t> shape, torch::ScalarType t) {
+        for (auto& b : al.ts)
+            if (b.data_ptr() == p) return b.narrow(0, 0, L * (t == torch::kFloat32 ? 12 : 4)).view(t).view(shape);
+        TORCH_CHECK(false, "trace_bvh: output not found");
+        return torch::Tensor();
+    };
+    return {contrib, view(pt, {L, 1}, torch::kInt32), view(pos, {L, 3}, torch::kFloat32),
+            view(rid, {L, 1}, torch::kInt32)};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -695,6 +818,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("densification_stats", &densification_stats);
     m.def("densify_and_prune", &densify_and_prune);
     m.def("reset_opacity", &reset_opacity);
+    // BVH visibility tracer (§8f rank 4): the reference's bvh_tracing._C names + the leaf boxes
+    m.def("create_bvh", &create_bvh);
+    m.def("trace_bvh", &trace_bvh);
+    m.def("trace_bvh_opacity", &trace_bvh_opacity);
+    m.def("bvh_leaf_aabbs", &bvh_leaf_aabbs);
     m.def("profile_enable", [](int64_t n) { check(r3dg_profile_enable((int)n), "profile_enable"); });
     m.def("profile_read", [](int64_t kernel) {
         int c = 0;
