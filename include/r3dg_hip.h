@@ -361,11 +361,13 @@ int r3dg_bvh_build(int P, int32_t* nodes, float* aabbs, uint64_t* morton, r3dg_a
  * the Gaussians it meets (cov3D_inv: [P, 6] upper-triangular inverse covariance, the
  * get_inverse_covariance of gaussian_model.py:410-413). Outputs: num_contributes int32 [R],
  * rendered_opacity f32 [R] (0 and 0 once the transmittance drops below 0.9). num_gaussians = P of
- * the tree (2P-1 nodes); it bounds the traversal, so a malformed tree cannot hang the GPU. */
+ * the tree (2P-1 nodes); it bounds the traversal, so a malformed tree cannot hang the GPU.
+ * Scratch (128 B per Gaussian: packed node and Gaussian records) from scratch_alloc. */
 int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int32_t* nodes, const float* aabbs, const float* rays_o,
                            const float* rays_d, const float* means3D, const float* cov3D_inv,
                            const float* opacities, const float* normals, int32_t* num_contributes,
-                           float* rendered_opacity, r3dg_stream_t stream);
+                           float* rendered_opacity, r3dg_alloc_fn scratch_alloc, void* scratch_ctx,
+                           r3dg_stream_t stream);
 
 /* trace_bvh (bvh/src/bvh.cu:28-85, trace.cu:8-196): per ray the Gaussians of every crossed
  * subtree of <= 4 leaves, sorted by (ray, t); num_contributes int32 [R] is their count per ray.

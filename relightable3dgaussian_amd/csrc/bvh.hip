@@ -6,13 +6,14 @@
 // RayTracer.__init__ (bvh/__init__.py:29-59), which the reference runs as ~40 torch launches.
 //
 // MI355X design (not a translation of the thrust lambdas):
-//   * build = 6 launches + one rocPRIM radix sort on the caller's stream, no host syncs:
+//   * build = 5-7 launches + one rocPRIM radix sort on the caller's stream, no host syncs:
 //     partial bounds -> final bounds -> Morton codes (also snapshots the leaf boxes) ->
 //     stable 30-bit radix sort of (code, Gaussian) -> leaf rows + 61-bit keys ->
-//     Karras split per internal node (subtree counts come from the key range, no atomics) ->
-//     bottom-up box merge with one arrival counter per internal node (agent-scope fences, so the
-//     second child reads its sibling's box through L2, not a stale L1 line).
-//   * traces: one lane per ray, depth-first with a 64-entry stack. The 61-bit keys are distinct,
+//     segment tree over the sorted leaf boxes (log2(P)/8 launches) -> Karras split per internal
+//     node, whose subtree count is its key range's length and whose box is that range's merge
+//     (no atomics, no fences: see range_box).
+//   * traces: one lane per ray, depth-first with a 64-entry stack (32 entries in LDS), over
+//     64-B node / Gaussian records packed per call (bvh_pack_kernel). The 61-bit keys are distinct,
 //     so the tree depth is at most 61 and the stack can never overflow (the reference's 32-entry
 //     IndexStack can, trace.cuh:22-45, with a printf and an out-of-bounds write).
 //   * the arithmetic is the reference's, operation for operation, and this file is compiled with
@@ -163,18 +164,20 @@ __device__ __forceinline__ uint32_t expand_bits(uint32_t v) {  // construct.cu:6
 __global__ void __launch_bounds__(256) bvh_morton_kernel(int P, int n_partial, const float* __restrict__ partial,
                                                          const float* __restrict__ leaf, uint32_t* __restrict__ code,
                                                          uint32_t* __restrict__ index, float* __restrict__ leaf_copy) {
-    __shared__ Box whole;
-    if (threadIdx.x == 0) {
-        Box w{100000.f, 100000.f, 100000.f, -100000.f, -100000.f, -100000.f};
-        for (int k = 0; k < n_partial; ++k) w = merge(w, load_box(partial, k));
-        whole = w;
-    }
+    __shared__ Box red[256];  // n_partial <= 256 partial boxes, reduced cooperatively per block
+    red[threadIdx.x] = (int)threadIdx.x < n_partial
+                           ? load_box(partial, threadIdx.x)
+                           : Box{100000.f, 100000.f, 100000.f, -100000.f, -100000.f, -100000.f};
     __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = merge(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const Box b = load_box(leaf, i);
     store_box(leaf_copy, i, b);
-    const Box w = whole;
+    const Box w = red[0];
     // centroid: (upper + lower) * 0.5 in double, rounded to float -- exact as 0.5f in float
     float px = (b.ux + b.lx) * 0.5f, py = (b.uy + b.ly) * 0.5f, pz = (b.uz + b.lz) * 0.5f;
     px -= w.lx; py -= w.ly; pz -= w.lz;
@@ -208,13 +211,61 @@ __global__ void __launch_bounds__(256) bvh_leaf_rows_kernel(int P, const uint32_
     row[4] = 1;
 }
 
+// Internal-node boxes without a bottom-up climb. A Karras node covers the contiguous sorted
+// leaves [first, last], and min / max are exact, so its box is the merge of the leaf boxes in that
+// range -- the same bits the reference's pairwise child merges produce (construct.cu:231-264).
+// The range merge is answered from an implicit segment tree over the sorted leaves (heap order,
+// n = pow2 >= P; level above the leaves in seg[1..n), the leaves themselves are the aabbs rows):
+// log2(n)/8 launches build it, then every internal node merges <= 2 log2(n) boxes. This replaces
+// the reference's atomic climb, whose agent-scope fences flush the per-XCD L2 of MI355X on every
+// step (5.6 ms at 1M Gaussians measured).
+__device__ __forceinline__ Box box_identity() {
+    return Box{INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+}
+
+__device__ __forceinline__ Box seg_get(const float* seg, const float* leaf, int P, int n, int h) {
+    if (h < n) return load_box(seg, h);
+    return h - n < P ? load_box(leaf, h - n) : box_identity();
+}
+
+// one block: 256 consecutive nodes of the level starting at heap index in_lo (or all of them when
+// the level is narrower) -> the up to 8 levels above
+__global__ void __launch_bounds__(256) bvh_seg_level_kernel(int P, int n, int in_lo, const float* __restrict__ leaf,
+                                                            float* seg) {
+    __shared__ Box lv[256];
+    const int cnt = in_lo < 256 ? in_lo : 256;
+    const int first = in_lo + blockIdx.x * cnt;
+    if ((int)threadIdx.x < cnt) lv[threadIdx.x] = seg_get(seg, leaf, P, n, first + threadIdx.x);
+    __syncthreads();
+    for (int step = 1, w = cnt >> 1; w >= 1; ++step, w >>= 1) {
+        Box m;
+        if ((int)threadIdx.x < w) m = merge(lv[2 * threadIdx.x], lv[2 * threadIdx.x + 1]);
+        __syncthreads();
+        if ((int)threadIdx.x < w) {
+            lv[threadIdx.x] = m;
+            store_box(seg, (first >> step) + threadIdx.x, m);
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ Box range_box(const float* seg, const float* leaf, int P, int n, int first, int last) {
+    Box acc = box_identity();
+    for (int l = first + n, r = last + n + 1; l < r; l >>= 1, r >>= 1) {
+        if (l & 1) acc = merge(acc, seg_get(seg, leaf, P, n, l++));
+        if (r & 1) acc = merge(acc, seg_get(seg, leaf, P, n, --r));
+    }
+    return acc;
+}
+
 __device__ __forceinline__ int cub64(uint64_t a, uint64_t b) { return __clzll(a ^ b); }  // common_upper_bits
 
 // one internal node per lane: determine_range (construct.cu:55-115) + find_split (:117-146),
 // children and parent links (:207-229); the subtree leaf count is the range length, which is
 // what the reference's bottom-up atomicAdd chain (:240) accumulates.
-__global__ void __launch_bounds__(256) bvh_internal_kernel(int P, const uint64_t* __restrict__ key,
-                                                           int32_t* __restrict__ nodes) {
+__global__ void __launch_bounds__(256) bvh_internal_kernel(int P, int n, const uint64_t* __restrict__ key,
+                                                           int32_t* __restrict__ nodes, const float* __restrict__ seg,
+                                                           float* __restrict__ aabbs) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int n_int = P - 1;
     if (idx >= n_int) return;
@@ -272,29 +323,7 @@ __global__ void __launch_bounds__(256) bvh_internal_kernel(int P, const uint64_t
     row[4] = last - first + 1;
     nodes[5 * (size_t)lc_id] = idx;
     nodes[5 * (size_t)rc_id] = idx;
-}
-
-// bottom-up boxes (construct.cu:231-264): one lane per leaf climbs; the first child to arrive at
-// a node stops, the second merges both boxes and continues. Release fence before the arrival
-// counter, acquire fence after it (invalidates this CU's L1 before the sibling's box is read).
-__global__ void __launch_bounds__(256) bvh_bottom_up_kernel(int P, const int32_t* __restrict__ nodes,
-                                                            float* aabbs, int* __restrict__ arrivals) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
-    int node = P - 1 + i;
-    Box box = load_box(aabbs, node);
-    int parent = nodes[5 * (size_t)node];
-    while (parent != -1) {
-        __threadfence();
-        if (atomicAdd(arrivals + parent, 1) == 0) return;
-        __threadfence();
-        const int l = nodes[5 * (size_t)parent + 1], r = nodes[5 * (size_t)parent + 2];
-        const Box other = load_box(aabbs, l == node ? r : l);
-        box = l == node ? merge(box, other) : merge(other, box);
-        store_box(aabbs, parent, box);
-        node = parent;
-        parent = nodes[5 * (size_t)node];
-    }
+    store_box(aabbs, idx, range_box(seg, aabbs + 6 * (size_t)n_int, P, n, first, last));
 }
 
 // ---- traces ----------------------------------------------------------------------------------
@@ -314,52 +343,96 @@ __device__ __forceinline__ void push_children(const float* aabbs, int lid, int r
     }
 }
 
+// Trace layouts, packed per call from the reference's tables (one pass, 64 B per node and per
+// Gaussian, ~0.03 ms at 1M): a visited internal node costs ONE 64-B record (both child boxes and
+// both child references) instead of a 20-B row plus two 24-B boxes in three dependent rounds, and
+// a leaf costs one 64-B Gaussian record instead of four scattered arrays.
+//   node record k (internal node k): {lbox[6], rbox[6], lref, rref, -, -}; ref >= 0 is an
+//   internal node, ref < 0 is ~gaussian (a leaf: count <= 1, the reference's test)
+//   gaussian record g: {mean xyz, opacity, normal xyz, -, cov_inv[6], -, -}
+__global__ void __launch_bounds__(256) bvh_pack_kernel(int P, const int32_t* __restrict__ nodes,
+                                                       const float* __restrict__ aabbs, const float* __restrict__ means,
+                                                       const float* __restrict__ cov, const float* __restrict__ opac,
+                                                       const float* __restrict__ normals, float4* __restrict__ nrec,
+                                                       float4* __restrict__ grec) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < P - 1) {
+        const int l = nodes[5 * (size_t)i + 1], r = nodes[5 * (size_t)i + 2];
+        const Box bl = load_box(aabbs, l), br = load_box(aabbs, r);
+        const int lref = nodes[5 * (size_t)l + 4] <= 1 ? ~nodes[5 * (size_t)l + 3] : l;
+        const int rref = nodes[5 * (size_t)r + 4] <= 1 ? ~nodes[5 * (size_t)r + 3] : r;
+        float4* o = nrec + 4 * (size_t)i;
+        o[0] = make_float4(bl.lx, bl.ly, bl.lz, bl.ux);
+        o[1] = make_float4(bl.uy, bl.uz, br.lx, br.ly);
+        o[2] = make_float4(br.lz, br.ux, br.uy, br.uz);
+        o[3] = make_float4(__int_as_float(lref), __int_as_float(rref), 0.f, 0.f);
+    }
+    if (i < P) {
+        const float* c = cov + 6 * (size_t)i;
+        float4* o = grec + 4 * (size_t)i;
+        const float3 m = ld3(means, i), n = ld3(normals, i);
+        o[0] = make_float4(m.x, m.y, m.z, opac[i]);
+        o[1] = make_float4(n.x, n.y, n.z, 0.f);
+        o[2] = make_float4(c[0], c[1], c[2], c[3]);
+        o[3] = make_float4(c[4], c[5], 0.f, 0.f);
+    }
+}
+
 struct TraceOpacityArgs {
     int n_rays;
-    const int32_t* nodes;
-    const float* aabbs;
+    int root_leaf;  // P == 1: the root is the leaf of Gaussian 0
+    const float4* nrec;
+    const float4* grec;
     const float* rays_o;
     const float* rays_d;
-    const float* means;
-    const float* cov_inv;
-    const float* opacity;
-    const float* normals;
     int32_t* contrib;
     float* vis;
     int max_visits;  // 2 * nodes: a bound no valid tree reaches (each node is visited at most once)
 };
 
+constexpr int kLdsStack = 32;  // per-lane stack entries in LDS ([entry][lane]: conflict-free)
+
 // trace_bvh_opacity_cuda (trace.cu:199-286): transmittance along the ray through every Gaussian
 // whose box it crosses (front-facing normals, opacity >= 1/255, density maximum at t >= 0.01);
 // once it drops below 0.9 the ray is occluded: visibility 0 and contribute 0 (the reference
-// returns before storing its count into the zero-initialised output).
+// returns before storing its count into the zero-initialised output). Same visit order as the
+// reference (so the same product order); the stack lives in LDS, deeper entries (> 32, rare)
+// in a private overflow array.
 __global__ void __launch_bounds__(256) bvh_trace_opacity_kernel(TraceOpacityArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ int lstack[kLdsStack][256];
+    const int tid = threadIdx.x;
+    const int idx = blockIdx.x * blockDim.x + tid;
     if (idx >= a.n_rays) return;
     const float3 o = ld3(a.rays_o, idx), d = ld3(a.rays_d, idx);
-    int stack[kBvhStack];
+    int ostack[kBvhStack - kLdsStack];
     int sp = 0;
-    stack[sp++] = 0;
+    auto push = [&](int v) {
+        if (sp < kLdsStack) lstack[sp][tid] = v;
+        else if (sp < kBvhStack) ostack[sp - kLdsStack] = v;
+        if (sp < kBvhStack) ++sp;
+    };
+    push(a.root_leaf ? ~0 : 0);
     int count = 0, visits = 0;
     float T = 1.f;
     while (sp > 0) {
-        const int node = stack[--sp];
-        const int32_t* row = a.nodes + 5 * (size_t)node;
-        if (row[4] <= 1) {
-            const int g = row[3];
-            const float op = a.opacity[g];
-            if (op < 1.f / 255.f) continue;
-            const float3 n = ld3(a.normals, g);
-            if (n.x * d.x + n.y * d.y + n.z * d.z > 0) continue;
-            const float3 m = ld3(a.means, g);
-            const float* c = a.cov_inv + 6 * (size_t)g;
+        --sp;
+        const int ref = sp < kLdsStack ? lstack[sp][tid] : ostack[sp - kLdsStack];
+        if (ref < 0) {
+            const float4* g = a.grec + 4 * (size_t)(~ref);
+            const float4 g0 = g[0];
+            if (g0.w < 1.f / 255.f) continue;
+            const float4 g1 = g[1];
+            if (g1.x * d.x + g1.y * d.y + g1.z * d.z > 0) continue;
+            const float4 g2 = g[2], g3 = g[3];
+            const float c[6] = {g2.x, g2.y, g2.z, g2.w, g3.x, g3.y};
+            const float3 m = make_float3(g0.x, g0.y, g0.z);
             const float t = ray_gauss_t(m, c, o, d);
             if ((double)t < 0.01) continue;
             const float3 p = make_float3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
             const float power = gauss_power(m, p, c);
             if (power > 0) continue;
             count += 1;
-            const float alpha = op * __expf(power);
+            const float alpha = g0.w * __expf(power);
             T *= 1 - alpha;
             if ((double)T < 0.9) {
                 a.contrib[idx] = 0;
@@ -367,9 +440,18 @@ __global__ void __launch_bounds__(256) bvh_trace_opacity_kernel(TraceOpacityArgs
                 return;
             }
         } else {
-            push_children(a.aabbs, row[1], row[2], o, d, [&](int id, float2) {
-                if (sp < kBvhStack) stack[sp++] = id;
-            });
+            const float4* r = a.nrec + 4 * (size_t)ref;
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+            const float2 il = ray_box(Box{r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, o, d);
+            const float2 ir = ray_box(Box{r1.z, r1.w, r2.x, r2.y, r2.z, r2.w}, o, d);
+            const int lid = __float_as_int(r3.x), rid = __float_as_int(r3.y);
+            if (il.y > ir.y) {
+                if (il.y > 0) push(lid);
+                if (ir.y > 0) push(rid);
+            } else {
+                if (ir.y > 0) push(rid);
+                if (il.y > 0) push(lid);
+            }
         }
         if (++visits > a.max_visits) break;  // only a malformed tree gets here
     }
@@ -526,13 +608,15 @@ extern "C" int r3dg_bvh_build(int P, int32_t* nodes, float* aabbs, uint64_t* mor
     hipStream_t st = (hipStream_t)stream;
     const int n_int = P - 1;
     float* leaf = aabbs + 6 * (size_t)n_int;
-    const int n_partial = (int)std::min<long long>(1024, blocks(P));
+    const int n_partial = (int)std::min<long long>(256, blocks(P));
+    int n = 1;
+    while (n < P) n <<= 1;
     size_t sort_bytes = 0;
     R3DG_CHECK_HIP(rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                              (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)P, 0, 30, st));
     const size_t b_partial = align256(24 * (size_t)n_partial), b_u32 = align256(4 * (size_t)P),
-                 b_copy = align256(24 * (size_t)P), b_arr = align256(4 * (size_t)std::max(n_int, 1));
-    char* s = (char*)scratch_alloc(scratch_ctx, b_partial + 4 * b_u32 + b_copy + b_arr + align256(sort_bytes) + 256);
+                 b_copy = align256(24 * (size_t)P), b_seg = align256(24 * (size_t)n);
+    char* s = (char*)scratch_alloc(scratch_ctx, b_partial + 4 * b_u32 + b_copy + b_seg + align256(sort_bytes) + 256);
     R3DG_REQUIRE(s, "create_bvh: scratch allocation failed");
     s = (char*)(((uintptr_t)s + 255) & ~(uintptr_t)255);
     float* partial = (float*)s; s += b_partial;
@@ -541,7 +625,7 @@ extern "C" int r3dg_bvh_build(int P, int32_t* nodes, float* aabbs, uint64_t* mor
     uint32_t* code_s = (uint32_t*)s; s += b_u32;
     uint32_t* index_s = (uint32_t*)s; s += b_u32;
     float* leaf_copy = (float*)s; s += b_copy;
-    int* arrivals = (int*)s; s += b_arr;
+    float* seg = (float*)s; s += b_seg;
     void* tmp = s;
     hipLaunchKernelGGL(bvh_bounds_partial_kernel, dim3(n_partial), dim3(256), 0, st, P, leaf, partial);
     R3DG_CHECK_HIP(hipGetLastError());
@@ -554,29 +638,45 @@ extern "C" int r3dg_bvh_build(int P, int32_t* nodes, float* aabbs, uint64_t* mor
                        aabbs, morton);
     R3DG_CHECK_HIP(hipGetLastError());
     if (n_int > 0) {
-        R3DG_CHECK_HIP(hipMemsetAsync(arrivals, 0, 4 * (size_t)n_int, st));
-        hipLaunchKernelGGL(bvh_internal_kernel, dim3(blocks(n_int)), dim3(256), 0, st, P, morton, nodes);
-        R3DG_CHECK_HIP(hipGetLastError());
-        hipLaunchKernelGGL(bvh_bottom_up_kernel, dim3(blocks(P)), dim3(256), 0, st, P, nodes, aabbs, arrivals);
+        for (int in_lo = n; in_lo > 1;) {
+            const int cnt = in_lo < 256 ? in_lo : 256;
+            hipLaunchKernelGGL(bvh_seg_level_kernel, dim3(in_lo / cnt), dim3(256), 0, st, P, n, in_lo, leaf, seg);
+            R3DG_CHECK_HIP(hipGetLastError());
+            in_lo /= cnt;
+        }
+        hipLaunchKernelGGL(bvh_internal_kernel, dim3(blocks(n_int)), dim3(256), 0, st, P, n, morton, nodes, seg,
+                           aabbs);
         R3DG_CHECK_HIP(hipGetLastError());
     }
     return R3DG_OK;
 }
 
-extern "C" int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int32_t* nodes, const float* aabbs, const float* rays_o,
-                                      const float* rays_d, const float* means3D, const float* cov3D_inv,
-                                      const float* opacities, const float* normals, int32_t* num_contributes,
-                                      float* rendered_opacity, r3dg_stream_t stream) {
+extern "C" int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int32_t* nodes, const float* aabbs,
+                                      const float* rays_o, const float* rays_d, const float* means3D,
+                                      const float* cov3D_inv, const float* opacities, const float* normals,
+                                      int32_t* num_contributes, float* rendered_opacity, r3dg_alloc_fn scratch_alloc,
+                                      void* scratch_ctx, r3dg_stream_t stream) {
     R3DG_REQUIRE(num_rays >= 0, "trace_bvh_opacity: negative ray count");
     if (num_rays == 0) return R3DG_OK;
     R3DG_REQUIRE(num_gaussians >= 1, "trace_bvh_opacity: empty tree");
     R3DG_REQUIRE(nodes && aabbs && rays_o && rays_d && means3D && cov3D_inv && opacities && normals &&
-                     num_contributes && rendered_opacity,
+                     num_contributes && rendered_opacity && scratch_alloc,
                  "trace_bvh_opacity: null buffer");
     R3DG_REQUIRE(((uintptr_t)aabbs & 7) == 0, "trace_bvh_opacity: aabbs must be 8-B aligned");
-    TraceOpacityArgs a{num_rays, nodes, aabbs, rays_o, rays_d, means3D, cov3D_inv, opacities, normals,
-                       num_contributes, rendered_opacity, 2 * (2 * num_gaussians - 1)};
-    hipLaunchKernelGGL(bvh_trace_opacity_kernel, dim3(blocks(num_rays)), dim3(256), 0, (hipStream_t)stream, a);
+    hipStream_t st = (hipStream_t)stream;
+    const int P = num_gaussians;
+    const size_t b_n = align256(64 * (size_t)std::max(P - 1, 1)), b_g = align256(64 * (size_t)P);
+    char* s = (char*)scratch_alloc(scratch_ctx, b_n + b_g + 256);
+    R3DG_REQUIRE(s, "trace_bvh_opacity: scratch allocation failed");
+    s = (char*)(((uintptr_t)s + 255) & ~(uintptr_t)255);
+    float4* nrec = (float4*)s;
+    float4* grec = (float4*)(s + b_n);
+    hipLaunchKernelGGL(bvh_pack_kernel, dim3(blocks(P)), dim3(256), 0, st, P, nodes, aabbs, means3D, cov3D_inv,
+                       opacities, normals, nrec, grec);
+    R3DG_CHECK_HIP(hipGetLastError());
+    TraceOpacityArgs a{num_rays, P == 1 ? 1 : 0, nrec, grec, rays_o, rays_d, num_contributes, rendered_opacity,
+                       2 * (2 * P - 1)};
+    hipLaunchKernelGGL(bvh_trace_opacity_kernel, dim3(blocks(num_rays)), dim3(256), 0, st, a);
     R3DG_CHECK_HIP(hipGetLastError());
     return R3DG_OK;
 }

@@ -730,10 +730,11 @@ std::tuple<torch::Tensor, torch::Tensor> trace_bvh_opacity(const torch::Tensor& 
     TORCH_CHECK(P >= 1 && nd.numel() == 5 * (2 * P - 1) && bx.numel() == 6 * (2 * P - 1) && c.numel() == 6 * P &&
                     op.numel() == P && n.numel() == 3 * P,
                 "trace_bvh_opacity: tree / Gaussian shapes disagree");
+    TensorAlloc scratch{o.options().dtype(torch::kUInt8), {}};
     check(r3dg_bvh_trace_opacity((int)R, (int)P, nd.data_ptr<int32_t>(), bx.data_ptr<float>(), o.data_ptr<float>(),
                                  d.data_ptr<float>(), m.data_ptr<float>(), c.data_ptr<float>(), op.data_ptr<float>(),
                                  n.data_ptr<float>(), contrib.data_ptr<int32_t>(), vis.data_ptr<float>(),
-                                 stream_of(o.device())),
+                                 tensor_alloc, &scratch, stream_of(o.device())),
           "trace_bvh_opacity");
     return {contrib, vis};
 }
