@@ -154,6 +154,25 @@ class GaussianTrainState:
     def grad_view(self, name):
         return self._view(self.grad, name)
 
+    # ---- gaussian_model.py:658-793 (PLY checkpoints) -------------------------------------------
+    @staticmethod
+    def load_ply(path: str, device="cuda", use_pbr: bool = True, max_sh_degree: int = 3, **kw):
+        """load_ply (gaussian_model.py:693-793) straight into the flat parameter buffer."""
+        import torch
+
+        from .ply import load_ply
+
+        arrs = load_ply(path, max_sh_degree=max_sh_degree, use_pbr=use_pbr)
+        return GaussianTrainState.from_tensors({k: torch.from_numpy(v).to(device) for k, v in arrs.items()},
+                                               use_pbr=use_pbr, **kw)
+
+    def save_ply(self, path: str) -> None:
+        """save_ply (gaussian_model.py:658-686) from the flat parameter buffer."""
+        from .ply import save_ply
+
+        names = [n for n, _ in self.groups]
+        save_ply(path, {n: self.view(n) for n in names}, use_pbr="base_color" in names)
+
     # ---- gaussian_model.py:581-620 -------------------------------------------------------------
     def training_setup(self, training_args, spatial_lr_scale=1.0):
         a = training_args

@@ -173,3 +173,16 @@ def test_integration_shim_package():
             "import relightable3dgaussian_amd as r; assert _C is r._C; print('ok')")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
+
+
+def test_integration_shim_bvh_packages():
+    """integration/bvh and integration/bvh_tracing import under the reference's package names."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "integration")]))
+    code = ("from bvh import RayTracer; from bvh_tracing import _C; import relightable3dgaussian_amd as r; "
+            "assert _C is r._C and RayTracer is r.bvh.RayTracer; "
+            "assert all(hasattr(_C, n) for n in ('create_bvh', 'trace_bvh', 'trace_bvh_opacity')); print('ok')")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
