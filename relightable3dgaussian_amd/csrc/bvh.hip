@@ -20,6 +20,7 @@
 //     -ffp-contract=off (build.py) so the result is bit-identical to the C restatement
 //     oracle/r3dg_bvh.c (only the trace's exp differs: __expf as the reference).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "r3dg_common.h"
@@ -381,6 +382,7 @@ __global__ void __launch_bounds__(256) bvh_pack_kernel(int P, const int32_t* __r
 struct TraceOpacityArgs {
     int n_rays;
     int root_leaf;  // P == 1: the root is the leaf of Gaussian 0
+    int g_bits;     // 2^g_bits lanes per ray (same wave), 0..6
     const float4* nrec;
     const float4* grec;
     const float* rays_o;
@@ -391,19 +393,38 @@ struct TraceOpacityArgs {
 };
 
 constexpr int kLdsStack = 32;  // per-lane stack entries in LDS ([entry][lane]: conflict-free)
+constexpr float kLogCut = -0.10536052f - 1e-5f;  // log(0.9) minus a rounding margin
 
 // trace_bvh_opacity_cuda (trace.cu:199-286): transmittance along the ray through every Gaussian
 // whose box it crosses (front-facing normals, opacity >= 1/255, density maximum at t >= 0.01);
 // once it drops below 0.9 the ray is occluded: visibility 0 and contribute 0 (the reference
-// returns before storing its count into the zero-initialised output). Same visit order as the
-// reference (so the same product order); the stack lives in LDS, deeper entries (> 32, rare)
-// in a private overflow array.
+// returns before storing its count into the zero-initialised output). The stack lives in LDS,
+// deeper entries (> 32, rare) in a private overflow array.
+//
+// Few rays (the lambda_visibility loss traces 10k) cannot fill 256 CUs one lane per ray, and the
+// time is then the longest traversal's latency. So a ray gets G = 2^g_bits lanes of one wave:
+// lane j walks down g_bits levels along the bits of j (pruning as the reference does) and
+// traverses that subtree in the reference's order; the group multiplies its partial
+// transmittances and sums its counts. The cut is monotone (every factor is <= 1), so "the product
+// fell below 0.9" is the same event whatever the order: the group keeps a running log-domain sum
+// in LDS and every lane stops once it crosses the cut. Only the rounding of the product differs
+// from the reference's single chain (G = 1 keeps the reference's order exactly).
 __global__ void __launch_bounds__(256) bvh_trace_opacity_kernel(TraceOpacityArgs a) {
     __shared__ int lstack[kLdsStack][256];
+    __shared__ float lsum[256];  // per group: sum of log(1 - alpha) so far (-inf: cut)
     const int tid = threadIdx.x;
-    const int idx = blockIdx.x * blockDim.x + tid;
-    if (idx >= a.n_rays) return;
-    const float3 o = ld3(a.rays_o, idx), d = ld3(a.rays_d, idx);
+    const int gb = a.g_bits;
+    const int j = tid & ((1 << gb) - 1);
+    const int gid = tid >> gb;  // group slot in this block
+    const int ray = (int)((blockIdx.x * blockDim.x + tid) >> gb);
+    const bool live = ray < a.n_rays;
+    if (j == 0) lsum[gid] = 0.f;
+    __syncthreads();
+    float3 o = make_float3(0.f, 0.f, 0.f), d = make_float3(0.f, 0.f, 1.f);
+    if (live) {
+        o = ld3(a.rays_o, ray);
+        d = ld3(a.rays_d, ray);
+    }
     int ostack[kBvhStack - kLdsStack];
     int sp = 0;
     auto push = [&](int v) {
@@ -411,19 +432,39 @@ __global__ void __launch_bounds__(256) bvh_trace_opacity_kernel(TraceOpacityArgs
         else if (sp < kBvhStack) ostack[sp - kLdsStack] = v;
         if (sp < kBvhStack) ++sp;
     };
-    push(a.root_leaf ? ~0 : 0);
+    // descend g_bits levels along the bits of j; a leaf met early belongs to the lane whose
+    // remaining bits are zero, a pruned child to nobody
+    int ref = a.root_leaf ? ~0 : 0;
+    bool mine = live;
+    for (int lv = 0; lv < gb && mine; ++lv) {
+        if (ref < 0) {
+            mine = (j >> lv) == 0;
+            break;
+        }
+        const float4* r = a.nrec + 4 * (size_t)ref;
+        const int right = (j >> lv) & 1;
+        const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+        const float2 iv = right ? ray_box(Box{r1.z, r1.w, r2.x, r2.y, r2.z, r2.w}, o, d)
+                                : ray_box(Box{r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, o, d);
+        mine = iv.y > 0;
+        ref = __float_as_int(right ? r3.y : r3.x);
+    }
+    if (mine) push(ref);
     int count = 0, visits = 0;
     float T = 1.f;
+    bool occluded = false;
     while (sp > 0) {
+        // the group's running transmittance (log domain, LDS atomics) crossed the cut: stop. The
+        // 1e-5 margin keeps __logf rounding from cutting a ray whose exact product is >= 0.9;
+        // rays inside the margin finish their traversal and the exact product decides
+        if (gb > 0 && *(volatile float*)&lsum[gid] < kLogCut) break;
         --sp;
-        const int ref = sp < kLdsStack ? lstack[sp][tid] : ostack[sp - kLdsStack];
-        if (ref < 0) {
-            const float4* g = a.grec + 4 * (size_t)(~ref);
-            const float4 g0 = g[0];
+        const int rf = sp < kLdsStack ? lstack[sp][tid] : ostack[sp - kLdsStack];
+        if (rf < 0) {
+            const float4* g = a.grec + 4 * (size_t)(~rf);
+            const float4 g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3];  // one 64-B line, one round trip
             if (g0.w < 1.f / 255.f) continue;
-            const float4 g1 = g[1];
             if (g1.x * d.x + g1.y * d.y + g1.z * d.z > 0) continue;
-            const float4 g2 = g[2], g3 = g[3];
             const float c[6] = {g2.x, g2.y, g2.z, g2.w, g3.x, g3.y};
             const float3 m = make_float3(g0.x, g0.y, g0.z);
             const float t = ray_gauss_t(m, c, o, d);
@@ -435,12 +476,13 @@ __global__ void __launch_bounds__(256) bvh_trace_opacity_kernel(TraceOpacityArgs
             const float alpha = g0.w * __expf(power);
             T *= 1 - alpha;
             if ((double)T < 0.9) {
-                a.contrib[idx] = 0;
-                a.vis[idx] = 0.f;
-                return;
+                occluded = true;
+                if (gb > 0) lsum[gid] = -INFINITY;
+                break;
             }
+            if (gb > 0) atomicAdd(&lsum[gid], __logf(1 - alpha));
         } else {
-            const float4* r = a.nrec + 4 * (size_t)ref;
+            const float4* r = a.nrec + 4 * (size_t)rf;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
             const float2 il = ray_box(Box{r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, o, d);
             const float2 ir = ray_box(Box{r1.z, r1.w, r2.x, r2.y, r2.z, r2.w}, o, d);
@@ -455,8 +497,18 @@ __global__ void __launch_bounds__(256) bvh_trace_opacity_kernel(TraceOpacityArgs
         }
         if (++visits > a.max_visits) break;  // only a malformed tree gets here
     }
-    a.contrib[idx] = count;
-    a.vis[idx] = T;
+    if (gb > 0) {  // combine the group's partial results (butterfly within the wave)
+        for (int m = 1; m < (1 << gb); m <<= 1) {
+            T *= __shfl_xor(T, m, 64);
+            count += __shfl_xor(count, m, 64);
+        }
+        __syncthreads();  // every lane's updates are visible
+        occluded = lsum[gid] < kLogCut || (double)T < 0.9;
+    }
+    if (live && j == 0) {
+        a.contrib[ray] = occluded ? 0 : count;
+        a.vis[ray] = occluded ? 0.f : T;
+    }
 }
 
 struct TraceListArgs {
@@ -674,9 +726,20 @@ extern "C" int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int
     hipLaunchKernelGGL(bvh_pack_kernel, dim3(blocks(P)), dim3(256), 0, st, P, nodes, aabbs, means3D, cov3D_inv,
                        opacities, normals, nrec, grec);
     R3DG_CHECK_HIP(hipGetLastError());
-    TraceOpacityArgs a{num_rays, P == 1 ? 1 : 0, nrec, grec, rays_o, rays_d, num_contributes, rendered_opacity,
-                       2 * (2 * P - 1)};
-    hipLaunchKernelGGL(bvh_trace_opacity_kernel, dim3(blocks(num_rays)), dim3(256), 0, st, a);
+    // lanes per ray: enough lanes in flight to cover the chip (256 CUs x 4 SIMDs x ~5 waves),
+    // at most one wave per ray and never more lanes than the tree has depth-g_bits subtrees to
+    // hand out; R3DG_BVH_LANES overrides (1, 2, 4, ... 64) for measurements
+    int g_bits = 0;
+    const long long target = 256ll * 4 * 5 * 64;
+    while (g_bits < 6 && (long long)num_rays << (g_bits + 1) <= target && (2ll << g_bits) <= P) ++g_bits;
+    if (const char* e = getenv("R3DG_BVH_LANES")) {
+        const int want = atoi(e);
+        g_bits = 0;
+        while (g_bits < 6 && (2 << g_bits) <= want) ++g_bits;
+    }
+    TraceOpacityArgs a{num_rays, P == 1 ? 1 : 0, g_bits, nrec, grec, rays_o, rays_d, num_contributes,
+                       rendered_opacity, 2 * (2 * P - 1)};
+    hipLaunchKernelGGL(bvh_trace_opacity_kernel, dim3(blocks((long long)num_rays << g_bits)), dim3(256), 0, st, a);
     R3DG_CHECK_HIP(hipGetLastError());
     return R3DG_OK;
 }

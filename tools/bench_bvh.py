@@ -9,7 +9,12 @@ Also times the reference's own torch formulation of the leaf boxes (the ~40 elem
 bvh/__init__.py:29-59, restated here with torch on the same GPU) beside the one-launch kernel,
 and the C oracle's trace on a bounded ray sample as the CPU baseline (1 thread).
 
-Usage: python tools/bench_bvh.py [--P 1000000] [--rays 1000000] [--iters 10] [--out file.json]
+Scenes: "volume" (tests/test_bvh.py scene: 1M Gaussians filling a cube -- every ray is blocked
+within a short distance, a worst case for traversal length) and "surface" (Gaussians on sphere
+shells, flattened along their outward normals: the geometry the visibility term is meant for).
+
+Usage: python tools/bench_bvh.py [--P 1000000] [--rays 1000000] [--iters 10] [--scene volume|surface]
+                                 [--out file.json]
 """
 from __future__ import annotations
 
@@ -52,6 +57,33 @@ def torch_leaf_boxes(means3D, scales, rotations):
     return torch.cat([lo, hi], -1)
 
 
+def surface_scene(P, seed=0):
+    """Gaussians on the shells of 12 spheres, flattened along the outward normal (a surface-like
+    scene: rays from the centres into the normal's hemisphere either escape or hit another shell)."""
+    import oracle
+
+    rng = np.random.default_rng(seed)
+    centers = rng.uniform(-1.0, 1.0, (12, 3))
+    radii = rng.uniform(0.15, 0.4, 12)
+    k = rng.integers(0, 12, P)
+    n = rng.normal(size=(P, 3))
+    n /= np.linalg.norm(n, axis=1, keepdims=True)
+    means = centers[k] + radii[k, None] * n
+    s = np.exp(rng.uniform(np.log(0.004), np.log(0.015), (P, 1)))
+    scales = np.concatenate([s, s, 0.1 * s], axis=1)
+    # quaternion (w, x, y, z) rotating +z onto n
+    z = np.array([0.0, 0.0, 1.0])
+    axis = np.cross(np.broadcast_to(z, n.shape), n)
+    w = 1.0 + n[:, 2]
+    q = np.concatenate([w[:, None], axis], axis=1)
+    q[w < 1e-6] = [0.0, 1.0, 0.0, 0.0]
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    f = lambda a: np.ascontiguousarray(a, dtype=np.float32)  # noqa: E731
+    sc = dict(means=f(means), scales=f(scales), rots=f(q), opacity=f(rng.uniform(0.3, 0.95, P)), normals=f(n))
+    sc["cov_inv"] = f(oracle.cov3d(1.0 / sc["scales"], sc["rots"]))
+    return sc
+
+
 def timed(fn, iters, stream=None):
     for _ in range(2):
         fn()
@@ -74,6 +106,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--cpu-rays", type=int, default=20000)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--scene", choices=["volume", "surface"], default="volume")
     args = ap.parse_args()
     import oracle
     import relightable3dgaussian_amd as r3
@@ -81,11 +114,11 @@ def main():
     from tests.test_bvh import rays_from, scene
 
     torch.cuda.set_device(0)
-    sc = scene(args.P, seed=8, spread=1.0)
+    sc = scene(args.P, seed=8, spread=1.0) if args.scene == "volume" else surface_scene(args.P, seed=8)
     dev = lambda a: torch.as_tensor(a, device="cuda")  # noqa: E731
     means, scales, rots = dev(sc["means"]), dev(sc["scales"]), dev(sc["rots"])
     cov, opac, normals = dev(sc["cov_inv"]), dev(sc["opacity"]), dev(sc["normals"])
-    res = {"P": args.P, "rays": args.rays, "device": torch.cuda.get_device_name(0)}
+    res = {"P": args.P, "rays": args.rays, "scene": args.scene, "device": torch.cuda.get_device_name(0)}
     res["leaf_boxes_kernel_ms"] = timed(lambda: r3._C.bvh_leaf_aabbs(means, scales, rots), args.iters)
     res["leaf_boxes_torch_ms"] = timed(lambda: torch_leaf_boxes(means, scales, rots), args.iters)
     res["build_ms"] = timed(lambda: RayTracer(means, scales, rots), args.iters)
