@@ -12,7 +12,7 @@
 //     segment tree over the sorted leaf boxes (log2(P)/8 launches) -> Karras split per internal
 //     node, whose subtree count is its key range's length and whose box is that range's merge
 //     (no atomics, no fences: see range_box).
-//   * traces: one lane per ray, depth-first with a 64-entry stack (32 entries in LDS), over
+//   * traces: one lane per ray, depth-first with a 64-entry stack (16 entries in LDS), over
 //     64-B node / Gaussian records packed per call (bvh_pack_kernel). The 61-bit keys are distinct,
 //     so the tree depth is at most 61 and the stack can never overflow (the reference's 32-entry
 //     IndexStack can, trace.cuh:22-45, with a printf and an out-of-bounds write).
@@ -392,14 +392,17 @@ struct TraceOpacityArgs {
     int max_visits;  // 2 * nodes: a bound no valid tree reaches (each node is visited at most once)
 };
 
-constexpr int kLdsStack = 32;  // per-lane stack entries in LDS ([entry][lane]: conflict-free)
+#ifndef R3DG_BVH_LDS
+#define R3DG_BVH_LDS 16  // measured: 8 / 12 / 16 / 24 / 32 entries (tools/exp_bvh.sh); 16 fills 7 waves per SIMD
+#endif
+constexpr int kLdsStack = R3DG_BVH_LDS;  // per-lane stack entries in LDS ([entry][lane]: conflict-free)
 constexpr float kLogCut = -0.10536052f - 1e-5f;  // log(0.9) minus a rounding margin
 
 // trace_bvh_opacity_cuda (trace.cu:199-286): transmittance along the ray through every Gaussian
 // whose box it crosses (front-facing normals, opacity >= 1/255, density maximum at t >= 0.01);
 // once it drops below 0.9 the ray is occluded: visibility 0 and contribute 0 (the reference
 // returns before storing its count into the zero-initialised output). The stack lives in LDS,
-// deeper entries (> 32, rare) in a private overflow array.
+// deeper entries (> 16) in a private overflow array (scratch, L1/L2-cached).
 //
 // Few rays (the lambda_visibility loss traces 10k) cannot fill 256 CUs one lane per ray, and the
 // time is then the longest traversal's latency. So a ray gets G = 2^g_bits lanes of one wave:
