@@ -514,6 +514,138 @@ __global__ void __launch_bounds__(256) bvh_trace_opacity_kernel(TraceOpacityArgs
     }
 }
 
+// Few-rays variant with dynamic balancing: the G lanes of a ray's group share one LDS stack
+// (kShared entries per lane). Every round each idle lane (empty private stack) pops one entry from
+// the top of the shared stack, all lanes process their node, and the children are pushed back in
+// lane order through a group prefix sum (pushes that do not fit go to the pushing lane's private
+// stack, which it drains first). Uniform per group: the stack pointer lives in a register of every
+// lane of the group, so no LDS atomics or barriers are needed -- a group never leaves its wave.
+// The subtree split of bvh_trace_opacity_kernel leaves most of an escaping ray's work in the one
+// subtree around its origin; here every lane keeps taking the next pending node.
+constexpr int kShared = 16;
+
+__device__ __forceinline__ int group_incl_scan(int v, int width) {
+    for (int o = 1; o < width; o <<= 1) {
+        const int u = __shfl_up(v, o, width);
+        if ((threadIdx.x & (width - 1)) >= o) v += u;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(256) bvh_trace_opacity_shared_kernel(TraceOpacityArgs a) {
+    __shared__ int sstack[256 * kShared];
+    __shared__ float lsum[256];
+    const int tid = threadIdx.x;
+    const int gb = a.g_bits, G = 1 << gb;
+    const int j = tid & (G - 1);
+    const int gid = tid >> gb;
+    const int lane = tid & 63;
+    const uint64_t gmask = G == 64 ? ~0ull : (((1ull << G) - 1) << (lane & ~(G - 1)));
+    const uint64_t below = (1ull << lane) - 1;
+    const int ray = (int)((blockIdx.x * blockDim.x + tid) >> gb);
+    const bool live = ray < a.n_rays;
+    const int C = kShared * G;
+    int* st = sstack + gid * C;
+    if (j == 0) lsum[gid] = 0.f;
+    float3 o = make_float3(0.f, 0.f, 0.f), d = make_float3(0.f, 0.f, 1.f);
+    if (live) {
+        o = ld3(a.rays_o, ray);
+        d = ld3(a.rays_d, ray);
+    }
+    int pstack[kBvhStack];
+    int psp = 0;
+    int sp = live ? 1 : 0;  // uniform within the group
+    if (live && j == 0) st[0] = a.root_leaf ? ~0 : 0;
+    int count = 0, visits = 0;
+    float T = 1.f;
+    bool occluded = false;
+    while (true) {
+        const uint64_t busy = __ballot(psp > 0) & gmask;
+        if (sp == 0 && busy == 0) break;
+        if (*(volatile float*)&lsum[gid] < kLogCut) break;
+        const uint64_t idle = ~busy & gmask;
+        const int n_idle = __popcll(idle), rank = __popcll(idle & below);
+        const int take = sp < n_idle ? sp : n_idle;
+        bool have = false;
+        int rf = 0;
+        if (psp > 0) {
+            rf = pstack[--psp];
+            have = true;
+        } else if (rank < take) {
+            rf = st[sp - 1 - rank];
+            have = true;
+        }
+        sp -= take;
+        int e0 = 0, e1 = 0, nc = 0;  // children to push, e1 ends on top
+        if (have) {
+            ++visits;
+            if (rf < 0) {
+                const float4* g = a.grec + 4 * (size_t)(~rf);
+                const float4 g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3];
+                bool hit = !(g0.w < 1.f / 255.f) && !(g1.x * d.x + g1.y * d.y + g1.z * d.z > 0);
+                const float c[6] = {g2.x, g2.y, g2.z, g2.w, g3.x, g3.y};
+                const float3 m = make_float3(g0.x, g0.y, g0.z);
+                float t = 0.f;
+                if (hit) {
+                    t = ray_gauss_t(m, c, o, d);
+                    hit = !((double)t < 0.01);
+                }
+                if (hit) {
+                    const float3 p = make_float3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
+                    const float power = gauss_power(m, p, c);
+                    if (!(power > 0)) {
+                        count += 1;
+                        const float alpha = g0.w * __expf(power);
+                        T *= 1 - alpha;
+                        if ((double)T < 0.9) {
+                            occluded = true;
+                            lsum[gid] = -INFINITY;
+                        } else {
+                            atomicAdd(&lsum[gid], __logf(1 - alpha));
+                        }
+                    }
+                }
+            } else {
+                const float4* r = a.nrec + 4 * (size_t)rf;
+                const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+                const float2 il = ray_box(Box{r0.x, r0.y, r0.z, r0.w, r1.x, r1.y}, o, d);
+                const float2 ir = ray_box(Box{r1.z, r1.w, r2.x, r2.y, r2.z, r2.w}, o, d);
+                const int lid = __float_as_int(r3.x), rid = __float_as_int(r3.y);
+                const bool lfirst = il.y > ir.y;  // the reference's push order
+                const int f = lfirst ? lid : rid, s2 = lfirst ? rid : lid;
+                const bool hf = lfirst ? il.y > 0 : ir.y > 0, hs = lfirst ? ir.y > 0 : il.y > 0;
+                if (hf) e0 = f;
+                if (hs) {
+                    if (hf) e1 = s2;
+                    else e0 = s2;
+                }
+                nc = (hf ? 1 : 0) + (hs ? 1 : 0);
+            }
+        }
+        const int incl = group_incl_scan(nc, G);
+        const int total = __shfl(incl, G - 1, G);
+        const int room = C - sp;
+        for (int k = 0; k < nc; ++k) {
+            const int pos = incl - nc + k;
+            const int e = k == 0 ? e0 : e1;
+            if (pos < room) st[sp + pos] = e;
+            else if (psp < kBvhStack) pstack[psp++] = e;
+        }
+        sp += total < room ? total : room;
+        if (visits > a.max_visits) psp = 0, sp = 0;  // only a malformed tree gets here
+    }
+    for (int m = 1; m < G; m <<= 1) {
+        T *= __shfl_xor(T, m, 64);
+        count += __shfl_xor(count, m, 64);
+    }
+    occluded = occluded || lsum[gid] < kLogCut || (double)T < 0.9;
+    occluded = __ballot(occluded) & gmask;
+    if (live && j == 0) {
+        a.contrib[ray] = occluded ? 0 : count;
+        a.vis[ray] = occluded ? 0.f : T;
+    }
+}
+
 struct TraceListArgs {
     int n_rays;
     const int32_t* nodes;
@@ -729,12 +861,12 @@ extern "C" int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int
     hipLaunchKernelGGL(bvh_pack_kernel, dim3(blocks(P)), dim3(256), 0, st, P, nodes, aabbs, means3D, cov3D_inv,
                        opacities, normals, nrec, grec);
     R3DG_CHECK_HIP(hipGetLastError());
-    // lanes per ray: enough lanes in flight to cover the chip (256 CUs x 4 SIMDs x ~5 waves),
-    // at most one wave per ray and never more lanes than the tree has depth-g_bits subtrees to
-    // hand out; R3DG_BVH_LANES overrides (1, 2, 4, ... 64) for measurements
-    int g_bits = 0;
-    const long long target = 256ll * 4 * 5 * 64;
-    while (g_bits < 6 && (long long)num_rays << (g_bits + 1) <= target && (2ll << g_bits) <= P) ++g_bits;
+    // lanes per ray (one wave's group, shared LDS stack): measured on 1M-Gaussian scenes
+    // (tools/gpu_bvh_lanes*.sh), 32 lanes is best or near-best from 100k to 1M rays (1M rays:
+    // 24.2 / 14.2 / 13.2 / 10.5 / 9.2 / 8.8 / 10.6 ms at 1 / 2 / ... / 64 lanes, volume scene), 64
+    // below ~32k rays; never more lanes than Gaussians. R3DG_BVH_LANES overrides (1, 2, 4, ... 64)
+    int g_bits = num_rays <= 32768 ? 6 : 5;
+    while (g_bits > 0 && (1ll << g_bits) > P) --g_bits;
     if (const char* e = getenv("R3DG_BVH_LANES")) {
         const int want = atoi(e);
         g_bits = 0;
@@ -742,7 +874,13 @@ extern "C" int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int
     }
     TraceOpacityArgs a{num_rays, P == 1 ? 1 : 0, g_bits, nrec, grec, rays_o, rays_d, num_contributes,
                        rendered_opacity, 2 * (2 * P - 1)};
-    hipLaunchKernelGGL(bvh_trace_opacity_kernel, dim3(blocks((long long)num_rays << g_bits)), dim3(256), 0, st, a);
+    // G > 1: shared-stack groups (R3DG_BVH_SPLIT=1: the static subtree split, for comparison)
+    const char* split = getenv("R3DG_BVH_SPLIT");
+    if (g_bits > 0 && !(split && atoi(split) == 1))
+        hipLaunchKernelGGL(bvh_trace_opacity_shared_kernel, dim3(blocks((long long)num_rays << g_bits)), dim3(256), 0,
+                           st, a);
+    else
+        hipLaunchKernelGGL(bvh_trace_opacity_kernel, dim3(blocks((long long)num_rays << g_bits)), dim3(256), 0, st, a);
     R3DG_CHECK_HIP(hipGetLastError());
     return R3DG_OK;
 }
