@@ -138,6 +138,52 @@ def brdf_c1(dev) -> dict:
             "sample": "oracle/brdf_torch.py: PyTorch-CPU restatement of gaussian_renderer/neilf.py:437-519"}
 
 
+def bvh_visibility(means3D, scales, rots, dev) -> dict:
+    """The BVH visibility tracer on the M1 Gaussians: RayTracer build and
+    trace_visibility of 10k rays (the lambda_visibility loss, neilf.py:323-348) and of one ray per
+    Gaussian (finetune_visibility, gaussian_model.py:446-465), rays from Gaussian centres into the
+    hemisphere of a random unit normal (M1 has no normals). Median of 5, HIP events."""
+    import torch
+
+    from relightable3dgaussian_amd.bvh import RayTracer
+
+    P = means3D.shape[0]
+    g = torch.Generator(device=dev).manual_seed(3)
+    normals = torch.nn.functional.normalize(torch.randn(P, 3, device=dev, generator=g), dim=1)
+    q = torch.nn.functional.normalize(rots, dim=1)
+    w, x, y, z = q.unbind(1)
+    R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                     2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                     2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], 1).view(P, 3, 3)
+    Sinv = R @ torch.diag_embed(1.0 / scales ** 2) @ R.transpose(1, 2)  # get_inverse_covariance
+    cov_inv = Sinv[:, [0, 0, 0, 1, 1, 2], [0, 1, 2, 1, 2, 2]].contiguous()
+    opac = torch.full((P, 1), 0.5, device=dev)
+
+    def med(fn, n=5):
+        fn()
+        ts = []
+        for _ in range(n):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        return float(np.median(ts))
+
+    res = {"gaussians": P, "build_ms": round(med(lambda: RayTracer(means3D, scales, rots)), 4)}
+    rt = RayTracer(means3D, scales, rots)
+    for R_, key in ((10000, "trace_10k"), (P, "trace_all")):
+        idx = torch.randint(0, P, (R_,), device=dev, generator=g) if R_ < P else torch.arange(P, device=dev)
+        o = means3D[idx].contiguous()
+        d = torch.randn(R_, 3, device=dev, generator=g)
+        d = torch.where(((d * normals[idx]).sum(1, keepdim=True) < 0), -d, d).contiguous()
+        res[key + "_ms"] = round(med(lambda: rt.trace_visibility(o, d, means3D, cov_inv, opac, normals)), 4)
+        res[key + "_mean_visibility"] = round(float(rt.trace_visibility(o, d, means3D, cov_inv, opac,
+                                                                        normals)["visibility"].mean()), 4)
+    return res
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -266,6 +312,8 @@ def main() -> None:
                      "algorithmic_bytes": bf + bb, "kernel_ms": round(t_kern * 1e3, 4)},
         "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
     }
+    if world == 1:
+        res["bvh_visibility"] = bvh_visibility(means3D, scales, rots, dev)
     if not args.no_cpu_baseline and world == 1:
         res["cpu_baseline"] = cpu_baseline(scene)
         res["brdf_cpu_baseline"] = brdf_c1(dev)
