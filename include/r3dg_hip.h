@@ -362,7 +362,8 @@ int r3dg_bvh_build(int P, int32_t* nodes, float* aabbs, uint64_t* morton, r3dg_a
  * get_inverse_covariance of gaussian_model.py:410-413). Outputs: num_contributes int32 [R],
  * rendered_opacity f32 [R] (0 and 0 once the transmittance drops below 0.9). num_gaussians = P of
  * the tree (2P-1 nodes); it bounds the traversal, so a malformed tree cannot hang the GPU.
- * Scratch (128 B per Gaussian: packed node and Gaussian records) from scratch_alloc. */
+ * Scratch from scratch_alloc: 128 B per Gaussian (packed node and Gaussian records), plus 16 B per
+ * ray and a radix-sort workspace when the rays are traced in Morton order (>= 256k rays). */
 int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int32_t* nodes, const float* aabbs, const float* rays_o,
                            const float* rays_d, const float* means3D, const float* cov3D_inv,
                            const float* opacities, const float* normals, int32_t* num_contributes,

@@ -338,19 +338,37 @@ __device__ __forceinline__ float3 surface_point(const XyzNormalArgs& a, int x, i
 }
 
 __global__ void __launch_bounds__(256) xyz_normal_kernel(XyzNormalArgs a) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    // the block's 18x18 neighbourhood (edge-clamped) of surface points, each evaluated once into
+    // LDS instead of nine times per pixel
+    __shared__ float sp[3][18 * 18];
+    const int bx = blockIdx.x * 16, by = blockIdx.y * 16;
+    for (int k = threadIdx.x; k < 18 * 18; k += 256) {
+        const int hx = min(max(bx + k % 18 - 1, 0), a.W - 1), hy = min(max(by + k / 18 - 1, 0), a.H - 1);
+        const float3 q = surface_point(a, hx, hy);
+        sp[0][k] = q.x;
+        sp[1][k] = q.y;
+        sp[2][k] = q.z;
+    }
+    __syncthreads();
+    const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+    const int x = bx + lx, y = by + ly;
     if (x >= a.W || y >= a.H) return;
     const int pix = y * a.W + x;
-    const int ym = y == 0 ? 0 : y - 1, yp = y == a.H - 1 ? a.H - 1 : y + 1;
-    const int xm = x == 0 ? 0 : x - 1, xp = x == a.W - 1 ? a.W - 1 : x + 1;
-    const float3 c = surface_point(a, x, y);
+    // neighbour (dx, dy) of this pixel; edge clamping already happened in the halo load, except
+    // that a pixel on the image's last row / column inside the block must clamp to itself
+    const int xm = lx, xc = lx + 1, xp = x == a.W - 1 ? lx + 1 : lx + 2;
+    const int ym = ly, yc = ly + 1, yp = y == a.H - 1 ? ly + 1 : ly + 2;
+    auto P3 = [&](int hx, int hy) {
+        const int k = hy * 18 + hx;
+        return make_float3(sp[0][k], sp[1][k], sp[2][k]);
+    };
+    const float3 c = P3(xc, yc);
     a.xyz[3 * pix + 0] = c.x;
     a.xyz[3 * pix + 1] = c.y;
     a.xyz[3 * pix + 2] = c.z;
-    const float3 p00 = surface_point(a, xm, ym), p01 = surface_point(a, x, ym), p02 = surface_point(a, xp, ym);
-    const float3 p10 = surface_point(a, xm, y), p12 = surface_point(a, xp, y);
-    const float3 p20 = surface_point(a, xm, yp), p21 = surface_point(a, x, yp), p22 = surface_point(a, xp, yp);
+    const float3 p00 = P3(xm, ym), p01 = P3(xc, ym), p02 = P3(xp, ym);
+    const float3 p10 = P3(xm, yc), p12 = P3(xp, yc);
+    const float3 p20 = P3(xm, yp), p21 = P3(xc, yp), p22 = P3(xp, yp);
     float ga[3], gb[3];
     const float3 q00 = p00, q01 = p01, q02 = p02, q10 = p10, q12 = p12, q20 = p20, q21 = p21, q22 = p22;
     const float* f00 = &q00.x; const float* f01 = &q01.x; const float* f02 = &q02.x; const float* f10 = &q10.x;
