@@ -493,7 +493,9 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         feats = copy(g->features, (size_t)S * P);
         R3DG_CHECK_HIP(ce);
     }
-    if (P > 0) {
+    // InitializeStencil (rasterizer_impl.cu:203-209): only the shaders and the intermediate
+    // depth / stencil pass read the per-Gaussian stencils; the all-default path skips the launch
+    if (P > 0 && (sh_active || splat_active || !post_ids.empty())) {
         hipLaunchKernelGGL(init_stencil_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, geom.stencils,
                            geom.stencil_opacity);
         R3DG_CHECK_LAUNCH(s->debug, st);
