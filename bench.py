@@ -51,6 +51,46 @@ def load_traffic() -> dict | None:
         return json.load(f)
 
 
+VALU_PEAK = 256 * 4 * 16 * 2.4e9  # lane-instructions/s: 256 CUs x 4 SIMD16 x 2.4 GHz (one wave64 op = 4 cycles)
+
+
+def load_valu(P: int) -> dict | None:
+    """profiles/valu_latest.json (tools/make_valu.py): per launch of each blend kernel, the VALU
+    wave-instructions (PMC SQ_INSTS_VALU, MFMA excluded) and the evaluated pixel x instance pairs E
+    (R3DG_EXP_COUNT build: live wave-steps x 64 lanes)."""
+    path = os.path.join(ROOT, "profiles", "valu_latest.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d if d.get("config") == f"M1 P={P}" else None
+
+
+def valu_roofline(v: dict | None, launch_ms: dict) -> dict | None:
+    """The blend's compute bound (SURVEY.md §8d VALU cross-check): lane-instructions issued per
+    second over the live launch time, against the VALU issue peak."""
+    if not v:
+        return None
+    out = {"unit": "lane-instr/s", "peak": VALU_PEAK, "source": "profiles/valu_latest.json"}
+    tot_i, tot_t = 0.0, 0.0
+    for k in ("render_fwd", "render_bwd", "row_sum"):
+        if k not in v or not launch_ms.get(k):
+            continue
+        t = launch_ms[k] / 1e3
+        lanes = v[k]["valu_insts"] * 64
+        ent = {"valu_insts": v[k]["valu_insts"], "achieved": lanes / t, "frac": round(lanes / t / VALU_PEAK, 4)}
+        if v[k].get("evals"):
+            ent["evals"] = v[k]["evals"]
+            ent["ops_per_eval"] = round(lanes / v[k]["evals"], 2)
+        out[k] = ent
+        tot_i += lanes
+        tot_t += t
+    if tot_t > 0:
+        out["achieved"] = tot_i / tot_t
+        out["frac"] = round(tot_i / tot_t / VALU_PEAK, 4)
+    return out
+
+
 def cpu_baseline(scene) -> dict:
     """The CPU oracle (scalar C port of the reference path, one thread) on one full M1 step: the
     1M-Gaussian scene at 1920x1080, preprocess + sort + blend fwd + bwd (~20 s)."""
@@ -263,7 +303,7 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     prof = {k: _C.profile_read(i) for i, k in enumerate(["render_fwd", "render_bwd", "gather_bwd", "sort",
-                                                          "preprocess"])}
+                                                          "preprocess", "row_sum"])}
     _C.profile_enable(0)
     if world > 1:
         te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -281,12 +321,15 @@ def main() -> None:
     # per-step device time of each stage (sort = depth sort + tile sort: two scopes per step)
     avg = {k: v[1] / args.steps for k, v in prof.items()}
     launch = {k: (v[1] / v[0] if v[0] else float("nan")) for k, v in prof.items()}
-    t_kern = (launch["render_fwd"] + launch["render_bwd"]) / 1e3
+    # renderCUDA fwd + bwd: the backward blend AND its per-instance reduction (row_sum_kernel sums
+    # the partial rows the reference accumulates with atomics, backward.cu:552-611)
+    t_kern = (launch["render_fwd"] + launch["render_bwd"] + launch["row_sum"]) / 1e3
     achieved = (bf + bb) / t_kern / 1e9
     traffic = None
     tr = load_traffic()
     if tr and tr.get("config") == f"M1 P={args.P}":
-        traffic = tr.get("render_fwd_bytes", 0) + tr.get("render_bwd_bytes", 0)
+        traffic = tr.get("render_fwd_bytes", 0) + tr.get("render_bwd_bytes", 0) + tr.get("row_sum_bytes", 0)
+    valu = valu_roofline(load_valu(args.P), launch)
     res = {
         "metric": "Mpix/s fwd+bwd, 1M Gaussians @1920x1080; views/s at 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -308,8 +351,8 @@ def main() -> None:
         "views_per_s": round(world * args.steps / elapsed, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "render_fwd_kernel + render_bwd_kernel (tile blend)",
-                     "algorithmic_bytes": bf + bb, "kernel_ms": round(t_kern * 1e3, 4)},
+                     "kernel": "renderCUDA fwd + bwd: render_fwd_kernel + render_bwd_mfma_kernel + row_sum_kernel",
+                     "algorithmic_bytes": bf + bb, "kernel_ms": round(t_kern * 1e3, 4), "valu": valu},
         "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
     }
     if world == 1:

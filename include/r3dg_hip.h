@@ -252,7 +252,7 @@ int r3dg_shader_manager_info(int64_t manager, int* n_shaders, int64_t* handles, 
  * r3dg_profile_read synchronises on the recorded events, returns the launch count and summed
  * device time in ms for one kernel, and resets that kernel's records. */
 enum { R3DG_PROF_RENDER_FWD = 0, R3DG_PROF_RENDER_BWD = 1, R3DG_PROF_GATHER_BWD = 2, R3DG_PROF_SORT = 3,
-       R3DG_PROF_PREPROCESS = 4, R3DG_PROF_KINDS = 5 };
+       R3DG_PROF_PREPROCESS = 4, R3DG_PROF_ROW_SUM = 5, R3DG_PROF_KINDS = 6 };
 int r3dg_profile_enable(int max_records);
 int r3dg_profile_read(int kernel, int* count, float* total_ms);
 

@@ -334,6 +334,25 @@ def rasterize_backward(fwd, dL_dcolor, dL_dopacity, dL_ddepth, dL_dfeature, colo
                 dL_dcov3D=dcov, dL_dsh=dsh, dL_dscales=dscale, dL_drotations=drot, dL_dconic=dconic)
 
 
+def expf(x):
+    """r3dg_expf, the blend's exp (forward.cu:477 / backward.cu:527), elementwise on float32."""
+    x = np.ascontiguousarray(x, np.float32).reshape(-1)
+    f = lib().r3dg_expf
+    f.restype = ctypes.c_float
+    f.argtypes = [ctypes.c_float]
+    return np.array([f(float(v)) for v in x], np.float32)
+
+
+def expf_accuracy(lo=-80.0, hi=0.0, stride=1):
+    """(max ulp error, n, correctly rounded count) of r3dg_expf against double exp over every
+    `stride`-th float in [lo, hi]."""
+    f = lib().oracle_expf_max_ulp
+    f.restype = ctypes.c_double
+    n, ex = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    m = f(ctypes.c_float(lo), ctypes.c_float(hi), ctypes.c_uint32(stride), ctypes.byref(n), ctypes.byref(ex))
+    return m, n.value, ex.value
+
+
 def mark_visible(means3D, view):
     means3D = _f(means3D)
     out = np.zeros(means3D.shape[0], np.uint8)

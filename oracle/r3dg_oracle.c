@@ -19,6 +19,13 @@
  * tests/golden/make_golden.py). The tile blend itself has no reference fixture (the
  * reference ships no tests), see DESIGN.md "Parity".
  *
+ * The blend's `power` and `exp(power)` (forward.cu:468-477, backward.cu:526-527) are the two
+ * places where the reference's bits are compiler/libdevice-defined (nvcc's FMA contraction; CUDA
+ * expf, <= 2 ulp). Both are stated here as ONE fixed sequence of IEEE f32 operations --
+ * gauss_power (a fixed FMA pattern) and r3dg_expf (<= 0.90 ulp over [-80, 0], see below) -- that
+ * the HIP kernels repeat operation for operation, so alpha, T, the early stop and n_contrib are
+ * bit-identical between the two.
+ *
  * Deliberate, documented deviations from the reference:
  *   - Stencil accumulator initialised to 0 (forward.cu:312 leaves it uninitialised).
  *   - dL_ddirect_shs accumulated sequentially (render_equation.cu:443-445 is a data race).
@@ -60,6 +67,60 @@ static void get_rect(float px, float py, int max_radius, int gx, int gy, int* rm
     rmin[1] = imin(gy, imax(0, (int)((py - (float)max_radius) / BY)));
     rmax[0] = imin(gx, imax(0, (int)((px + (float)max_radius + BX - 1) / BX)));
     rmax[1] = imin(gy, imax(0, (int)((py + (float)max_radius + BY - 1) / BY)));
+}
+
+/* forward.cu:468 / backward.cu:526: -0.5f * (a dx^2 + c dy^2) - b dx dy as one fixed FMA pattern
+ * (the HIP kernels' gauss_power, r3dg_common.h). */
+static float gauss_power(const float* co, float dx, float dy)
+{
+    const float q = fmaf(co[0] * dx, dx, (co[2] * dy) * dy);
+    return fmaf(-0.5f, q, -((co[1] * dx) * dy));
+}
+
+static uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+/* forward.cu:477 / backward.cu:527 exp(power): Cody-Waite reduction by ln2 (16 + 24-bit split),
+ * degree-6 polynomial for e^r (1 + r exact), 2^k by an integer add to the exponent field (the
+ * shifted kf holds k in its low bits, (0x4B400000 << 23) == 0 mod 2^32). Input clamped to
+ * [-80, 0]. Identical operation sequence to r3dg_common.h r3dg_expf. */
+float r3dg_expf(float x)
+{
+    x = fminf(fmaxf(x, -80.0f), 0.0f);
+    const float kf = fmaf(x, 0x1.715476p+0f, 0x1.8p+23f);
+    const float k = kf - 0x1.8p+23f;
+    float r = fmaf(k, -0x1.62e400p-1f, x);
+    r = fmaf(k, -0x1.7f7d1cp-20f, r);
+    float p = 0x1.6a959cp-10f;
+    p = fmaf(p, r, 0x1.123a0ap-7f);
+    p = fmaf(p, r, 0x1.555850p-5f);
+    p = fmaf(p, r, 0x1.555492p-3f);
+    p = fmaf(p, r, 0x1.fffffcp-2f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    return u2f(f2u(p) + (f2u(kf) << 23));
+}
+
+/* Accuracy check of r3dg_expf against double-precision exp over the floats x = lo, ... stepping
+ * `stride` bit patterns through [lo, hi] (both <= 0): max error in ulp of the float result and the
+ * count of correctly rounded results. */
+double oracle_expf_max_ulp(float lo, float hi, uint32_t stride, long long* n, long long* exact)
+{
+    double maxe = 0.0;
+    *n = 0;
+    *exact = 0;
+    const uint64_t end = f2u(lo);
+    for (uint64_t u = f2u(hi) | 0x80000000u; u <= end; u += stride) {
+        const float x = u2f((uint32_t)u);
+        const double e = exp((double)x);
+        const float y = r3dg_expf(x);
+        const double ulp = ldexp(1.0, ilogb(e) - 23);
+        const double err = fabs((double)y - e) / ulp;
+        if (err > maxe) maxe = err;
+        ++*n;
+        if (y == (float)e) ++*exact;
+    }
+    return maxe;
 }
 
 /* auxiliary.h:58-66 */
@@ -422,9 +483,9 @@ void oracle_render_forward(int W, int H, int S, const uint32_t* ranges, const ui
                         uint32_t id = point_list[k];
                         float dx = means2D[2 * id] - pfx, dy = means2D[2 * id + 1] - pfy;
                         const float* co = conic_opacity + 4 * id;
-                        float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                        float power = gauss_power(co, dx, dy);
                         if (power > 0.0f) continue;
-                        float alpha = fminf(0.99f, co[3] * expf(power));
+                        float alpha = fminf(0.99f, co[3] * r3dg_expf(power));
                         if (alpha < 1.0f / 255.0f) continue;
                         float test_T = T * (1 - alpha);
                         if (test_T < 0.0001f) break; /* done = true */
@@ -468,9 +529,9 @@ void oracle_render_intermediate(int W, int H, const uint32_t* ranges, const uint
                         uint32_t id = point_list[k];
                         float dx = means2D[2 * id] - (float)px, dy = means2D[2 * id + 1] - (float)py;
                         const float* co = conic_opacity + 4 * id;
-                        float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                        float power = gauss_power(co, dx, dy);
                         if (power > 0.0f) continue;
-                        float G = expf(power);
+                        float G = r3dg_expf(power);
                         float alpha = fminf(0.99f, co[3] * G);
                         float salpha = fminf(0.99f, stencil_opacity[id] * G);
                         if (alpha < 1.0f / 255.0f && salpha < 1.0f / 255.0f) continue;
@@ -572,9 +633,9 @@ void oracle_render_backward(int W, int H, int S, const uint32_t* ranges, const u
                         uint32_t id = point_list[k];
                         float dx = means2D[2 * id] - (float)px, dy = means2D[2 * id + 1] - (float)py;
                         const float* co = conic_opacity + 4 * id;
-                        float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                        float power = gauss_power(co, dx, dy);
                         if (power > 0.0f) continue;
-                        float G = expf(power);
+                        float G = r3dg_expf(power);
                         float alpha = fminf(0.99f, co[3] * G);
                         if (alpha < 1.0f / 255.0f) continue;
                         T = T / (1.f - alpha);

@@ -178,25 +178,97 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));  // MFMA accumulator 
 typedef float f32x2 __attribute__((ext_vector_type(2)));    // packed fp32 pair (v_pk_* ops)
 
 // Exponent of the 2D Gaussian at offset (dx, dy) from its centre: -0.5 (a dx^2 + c dy^2) - b dx dy
-// (forward.cu:478, backward.cu:530). One fixed FMA pattern, so every call site -- forward and
-// backward, first or second instance of an unrolled pair -- rounds identically.
-// The blend kernels stage each instance's conic in the exp2 domain once, so a per-pixel step
-// evaluates power * log2(e) = dx (A dx + B dy) + C dy^2 in 5 VALU ops and feeds v_exp_f32
-// directly (A = -log2(e)/2 a, B = -log2(e) b, C = -log2(e)/2 c): 3 fewer ops than gauss_power
-// followed by __expf. The sign tests (power > 0) are unchanged by the positive scale.
-__device__ __forceinline__ float4 exp2_conic(float4 co) {
-    constexpr float L2E = 1.4426950408889634f;
-    return make_float4(-0.5f * L2E * co.x, -L2E * co.y, -0.5f * L2E * co.z, co.w);
-}
-__device__ __forceinline__ float gauss_power2(float4 k, float dx, float dy) {
-#pragma clang fp contract(off)
-    return __builtin_fmaf(k.z * dy, dy, dx * __builtin_fmaf(k.y, dy, k.x * dx));
-}
-
+// (forward.cu:468, backward.cu:526). The reference's nvcc build contracts this expression into
+// FMAs (fmad is on by default; the pattern is the compiler's choice); here one fixed FMA
+// pattern, restated operation for operation by the oracle (oracle/r3dg_oracle.c gauss_power), so
+// every call site -- forward, backward, either instance of an unrolled pair -- and the oracle
+// produce the same bits, and the `power > 0` test resolves identically everywhere.
 __device__ __forceinline__ float gauss_power(float4 co, float dx, float dy) {
 #pragma clang fp contract(off)
     const float q = __builtin_fmaf(co.x * dx, dx, (co.z * dy) * dy);
     return __builtin_fmaf(-0.5f, q, -((co.y * dx) * dy));
+}
+
+// The blend's exp (forward.cu:477 / backward.cu:527 `exp(power)`, i.e. CUDA expf: <= 2 ulp,
+// implementation-defined bits). One bit-reproducible f32 statement shared with the oracle
+// (oracle/r3dg_oracle.c r3dg_expf, the same operations in the same order): k = rint(x / ln2)
+// by the 1.5 * 2^23 shift, Cody-Waite reduction r = x - k ln2 (ln2 split 16 + 24 bits, both
+// products exact / singly rounded by the FMAs), degree-6 polynomial for e^r with 1 + r exact,
+// scaling by 2^k as an integer add to the exponent field (the shifted kf carries k in its low
+// bits and (0x4B400000 << 23) == 0 mod 2^32). Max error 0.90 ulp over every float in [-80, 0],
+// correctly rounded on 99.54 % of them (tests/test_oracle.py pins the oracle's copy). Inputs
+// clamp to [-80, 0]: every consumer has power <= 0, and e^-80 lies far below the alpha
+// threshold. With it, alpha -- and so T, the early stop and n_contrib -- are bit-identical to
+// the oracle's (tests/test_gpu_parity.py asserts n_contrib equal).
+__device__ __forceinline__ float r3dg_expf(float x) {
+#pragma clang fp contract(off)
+    x = __builtin_amdgcn_fmed3f(x, -80.0f, 0.0f);
+    const float kf = __builtin_fmaf(x, 0x1.715476p+0f, 0x1.8p+23f);
+    const float k = kf - 0x1.8p+23f;
+    float r = __builtin_fmaf(k, -0x1.62e400p-1f, x);
+    r = __builtin_fmaf(k, -0x1.7f7d1cp-20f, r);
+    float p = 0x1.6a959cp-10f;
+    p = __builtin_fmaf(p, r, 0x1.123a0ap-7f);
+    p = __builtin_fmaf(p, r, 0x1.555850p-5f);
+    p = __builtin_fmaf(p, r, 0x1.555492p-3f);
+    p = __builtin_fmaf(p, r, 0x1.fffffcp-2f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    return __uint_as_float(__float_as_uint(p) + (__float_as_uint(kf) << 23));
+}
+
+// r3dg_expf on two values with packed f32 ops (v_pk_fma_f32 / v_pk_add_f32): per component the
+// same IEEE operations in the same order, so each result is bit-identical to r3dg_expf.
+__device__ __forceinline__ f32x2 r3dg_expf2(float x0, float x1) {
+#pragma clang fp contract(off)
+    const f32x2 x = {__builtin_amdgcn_fmed3f(x0, -80.0f, 0.0f), __builtin_amdgcn_fmed3f(x1, -80.0f, 0.0f)};
+    const f32x2 sh = {0x1.8p+23f, 0x1.8p+23f};
+    const f32x2 kf = __builtin_elementwise_fma(x, f32x2{0x1.715476p+0f, 0x1.715476p+0f}, sh);
+    const f32x2 k = kf - sh;
+    f32x2 r = __builtin_elementwise_fma(k, f32x2{-0x1.62e400p-1f, -0x1.62e400p-1f}, x);
+    r = __builtin_elementwise_fma(k, f32x2{-0x1.7f7d1cp-20f, -0x1.7f7d1cp-20f}, r);
+    f32x2 p = {0x1.6a959cp-10f, 0x1.6a959cp-10f};
+    p = __builtin_elementwise_fma(p, r, f32x2{0x1.123a0ap-7f, 0x1.123a0ap-7f});
+    p = __builtin_elementwise_fma(p, r, f32x2{0x1.555850p-5f, 0x1.555850p-5f});
+    p = __builtin_elementwise_fma(p, r, f32x2{0x1.555492p-3f, 0x1.555492p-3f});
+    p = __builtin_elementwise_fma(p, r, f32x2{0x1.fffffcp-2f, 0x1.fffffcp-2f});
+    p = __builtin_elementwise_fma(p, r, f32x2{1.0f, 1.0f});
+    p = __builtin_elementwise_fma(p, r, f32x2{1.0f, 1.0f});
+    return f32x2{__uint_as_float(__float_as_uint(p.x) + (__float_as_uint(kf.x) << 23)),
+                 __uint_as_float(__float_as_uint(p.y) + (__float_as_uint(kf.y) << 23))};
+}
+
+// Fast approximate exp for the backward's gradient values (v_exp_f32 on x * log2 e; ~4e-7
+// relative at |x| <= 6). Decisions never rest on it alone: see alpha_ok_bwd.
+__device__ __forceinline__ float fast_expf(float x) {
+    return __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
+}
+
+// The reference's alpha test `alpha < 1/255` (forward.cu:478, backward.cu:529) for the backward,
+// which must skip exactly the instances the forward skipped. oG = opacity * fast_expf(power);
+// its relative error is < 1e-6 for any alpha near the threshold (power >= ln(1/255) there), so
+// away from a 4e-6 band the decision equals the exact one; inside the band the step re-evaluates
+// with r3dg_expf (rare; one wave-uniform branch). Returns the exact-decision G.
+__device__ __forceinline__ float settle_threshold(float power, float opacity, float G) {
+    const bool near = fabsf(__builtin_fmaf(opacity * G, 255.0f, -1.0f)) < 4e-6f;
+#ifndef R3DG_NOSETTLE
+    if (__builtin_expect(__ballot(near) != 0ull, 0)) {
+        if (near) G = r3dg_expf(power);
+    }
+#else
+    (void)near;
+#endif
+    return G;
+}
+
+// settle_threshold for a pair of steps with one wave-uniform branch.
+__device__ __forceinline__ void settle_threshold2(float pw0, float o0, float& G0, float pw1, float o1, float& G1) {
+    const bool n0 = fabsf(__builtin_fmaf(o0 * G0, 255.0f, -1.0f)) < 4e-6f;
+    const bool n1 = fabsf(__builtin_fmaf(o1 * G1, 255.0f, -1.0f)) < 4e-6f;
+    if (__builtin_expect(__ballot(n0 || n1) != 0ull, 0)) {
+        if (n0) G0 = r3dg_expf(pw0);
+        if (n1) G1 = r3dg_expf(pw1);
+    }
 }
 
 // Minimum of Q(d) = a dx^2 + 2b dx dy + c dy^2 (positive definite) over mean - pixel offsets with

@@ -184,6 +184,7 @@ __global__ void intermediate_kernel(IntermediateArgs a);
 // host launchers for the templated blend kernels
 hipError_t launch_render_forward(const RenderFwdArgs& a, bool shader, hipStream_t stream);
 hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t stream);
+hipError_t launch_row_sum(const GatherBwdArgs& a, hipStream_t stream);
 hipError_t launch_gather_backward(const GatherBwdArgs& a, hipStream_t stream);
 
 // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so block b runs on the

@@ -815,15 +815,19 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     // per-Gaussian phase over n_chunks 256-aligned ranges; chunk_done after each range's launch
     const int nchunks = std::max(1, std::min(out->n_chunks, (P + 255) / 256));
     const int per = ((P + nchunks - 1) / nchunks + 255) & ~255;
-    {
-        ProfScope ps(R3DG_PROF_GATHER_BWD, st);
-        for (int c = 0, g0 = 0; g0 < P; ++c, g0 += per) {
-            ga.g_begin = g0;
-            ga.g_end = std::min(P, g0 + per);
-            R3DG_CHECK_HIP(launch_gather_backward(ga, st));
-            R3DG_CHECK_LAUNCH(s->debug, st);
-            if (out->chunk_done) out->chunk_done(out->chunk_ctx, c, ga.g_begin, ga.g_end);
+    for (int c = 0, g0 = 0; g0 < P; ++c, g0 += per) {
+        ga.g_begin = g0;
+        ga.g_end = std::min(P, g0 + per);
+        {
+            ProfScope ps(R3DG_PROF_ROW_SUM, st);
+            R3DG_CHECK_HIP(launch_row_sum(ga, st));
         }
+        {
+            ProfScope ps(R3DG_PROF_GATHER_BWD, st);
+            R3DG_CHECK_HIP(launch_gather_backward(ga, st));
+        }
+        R3DG_CHECK_LAUNCH(s->debug, st);
+        if (out->chunk_done) out->chunk_done(out->chunk_ctx, c, ga.g_begin, ga.g_end);
     }
     return R3DG_OK;
 }

@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
             const float4* rec = a.records + (size_t)gid * RF4;
             const float4 co = rec[0], r1 = rec[1];
             s_xy[t] = make_float2(r1.x, r1.y);
-            s_co[t] = exp2_conic(co);
+            s_co[t] = co;
             s_slot[t] = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
             s_mask[t] = quadrant_mask(make_float2(r1.x, r1.y), co, tx * kTileX, ty * kTileY, a.cull);
 #pragma unroll
@@ -133,11 +133,11 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
             if (contrib) {
                 const float2 xy = s_xy[j];
                 co = s_co[j];
-                const float power = gauss_power2(co, xy.x - pfx, xy.y - pfy);  // exp2-domain conic
+                const float power = gauss_power(co, xy.x - pfx, xy.y - pfy);
                 if (power > 0.0f) {
                     contrib = false;
                 } else {
-                    G = __builtin_amdgcn_exp2f(power);
+                    G = settle_threshold(power, co.w, fast_expf(power));
                     alpha = fminf(0.99f, co.w * G);
                     if (alpha < 1.0f / 255.0f) contrib = false;
                 }
@@ -228,9 +228,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef R3DG_BWD_NB
 #define R3DG_BWD_NB 64  // instances staged per batch
 #endif
-#ifndef R3DG_BWD_PF
-#define R3DG_BWD_PF 0  // 1: conic / position of the next instance pair read one iteration ahead
-#endif
 #ifndef R3DG_BWD_PKDOT
 #define R3DG_BWD_PKDOT 1  // the per-pixel channel dot as packed fp32 FMAs
 #endif
@@ -303,7 +300,6 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     // from the quadrant centre: x depends only on s2&1 and y = (s2>>1) - 3.5 is wave-uniform per
     // s2, so the B operand of k-step s2 is yA[s2&1] + y*(yB[s2&1] + y*yC) (exact: every term but
     // one is a zero product).
-    float yA[2], yB[2], yC;
     {
 #pragma unroll
         for (int xb = 0; xb < NXB; ++xb) {
@@ -321,14 +317,6 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
             wave_lds_sync();
         }
-        const int nch = l & 15;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const float xo = (float)(4 * h + (l >> 4)) - 3.5f;
-            yA[h] = nch == 0 ? 1.f : (nch == 1 ? xo : (nch == 3 ? xo * xo : 0.f));
-            yB[h] = nch == 2 ? 1.f : (nch == 4 ? xo : 0.f);
-        }
-        yC = nch == 5 ? 1.f : 0.f;
     }
 
     // The reference keeps one accum_rec per channel (colour, features, depth) and accum_opa; all
@@ -366,7 +354,8 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
     // One blend step of the reference's per-pixel loop (backward.cu:520-611), predicated rather
     // than branched: every LDS read is issued up front and a non-contributing pixel (outside,
     // past n_contrib, power > 0 or alpha < 1/255) leaves its state unchanged.
-    auto step = [&](int j, int p, bool live, float4 co, float2 xy, float& wv, float& qv) {
+    // `power` (the forward's bits) and G (fast exp, alpha test settled exactly) come from the caller.
+    auto step = [&](int j, int p, bool live, float opacity, float power, float G, float& wv, float& qv) {
 #pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
         const int ju = __builtin_amdgcn_readfirstlane(j);  // uniform addresses
         const float4* rj = s_rec + ju * SF4;
@@ -376,9 +365,7 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             const float4 rr = rj[1 + q];
             v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
         }
-        const float power = gauss_power2(co, xy.x - pfx, xy.y - pfy);  // exp2-domain conic
-        const float G = __builtin_amdgcn_exp2f(power);
-        const float alpha = fminf(0.99f, co.w * G);
+        const float alpha = fminf(0.99f, opacity * G);
         // p < last is false for pixels outside the image (last = 0 there)
         const bool ok = live && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
         const float ae = ok ? alpha : 0.f;
@@ -417,6 +404,16 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
 #ifdef R3DG_EXP_NOFLUSH  // timing experiment only: no flush products
         return;
 #endif
+        // the Y operand coefficients, rebuilt per flush from the lane id (5 fewer live VGPRs in
+        // the step loop)
+        float yA[2], yB[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float xo = (float)(4 * h + (l >> 4)) - 3.5f;
+            yA[h] = nch == 0 ? 1.f : (nch == 1 ? xo : (nch == 3 ? xo * xo : 0.f));
+            yB[h] = nch == 2 ? 1.f : (nch == 4 ? xo : 0.f);
+        }
+        const float yC = nch == 5 ? 1.f : 0.f;
         wave_lds_sync();
         floatx4 accX[NXB], accY = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -483,7 +480,7 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             for (int q = 0; q < RF4; ++q) rv[q] = rec[q];
             const int hn = hi - NB;
             gid_next = (hn > 0 && t < min(NB, hn)) ? a.point_list[range.x + (uint32_t)(hn - 1 - t)] : 0u;
-            s_rec[t * SF4] = exp2_conic(rv[0]);
+            s_rec[t * SF4] = rv[0];
 #pragma unroll
             for (int q = 0; q < NA4; ++q) s_rec[t * SF4 + 1 + q] = rv[2 + q];
             s_xy[t] = make_float2(rv[1].x, rv[1].y);
@@ -516,8 +513,7 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             else if (lo > 0) bits &= ~0u << lo;
             if (l == 0) R3DG_EXP_ADD(0, __builtin_popcount(bits));
             // two compacted instances per iteration: the second one's LDS reads and exp overlap
-            // the first one's dependent chain. R3DG_BWD_PF: the next pair's conic and position
-            // are read one iteration ahead, so a pair's chain does not start with an LDS wait.
+            // the first one's dependent chain
             auto take = [&](int& ja, int& jb, bool& hb) {
                 ja = c * 32 + __builtin_ctz(bits);
                 bits &= bits - 1;
@@ -527,38 +523,19 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
             };
             auto rec0 = [&](int j) { return s_rec[__builtin_amdgcn_readfirstlane(j) * SF4]; };
             auto pos = [&](int j) { return s_xy[__builtin_amdgcn_readfirstlane(j)]; };
-#if R3DG_BWD_PF
-            int j0 = 0, j1 = 0;
-            bool has1 = false;
-            float4 co0 = make_float4(0.f, 0.f, 0.f, 0.f), co1 = co0;
-            float2 xy0 = make_float2(0.f, 0.f), xy1 = xy0;
-            bool cur = bits != 0u;
-            if (cur) {
-                take(j0, j1, has1);
-                co0 = rec0(j0); co1 = rec0(j1); xy0 = pos(j0); xy1 = pos(j1);
-            }
-            while (cur) {
-                int n0 = 0, n1 = 0;
-                bool nh1 = false;
-                float4 nco0 = co0, nco1 = co1;
-                float2 nxy0 = xy0, nxy1 = xy1;
-                const bool nxt = bits != 0u;
-                if (nxt) {
-                    take(n0, n1, nh1);
-                    nco0 = rec0(n0); nco1 = rec0(n1); nxy0 = pos(n0); nxy1 = pos(n1);
-                }
-                float wv0, qv0, wv1, qv1;
-                step(j0, hi - 1 - j0, true, co0, xy0, wv0, qv0);
-                step(j1, hi - 1 - j1, has1, co1, xy1, wv1, qv1);
-#else
             while (bits) {
                 int j0, j1;
                 bool has1;
                 take(j0, j1, has1);
+                const float4 co0 = rec0(j0), co1 = rec0(j1);
+                const float2 xy0 = pos(j0), xy1 = pos(j1);
+                const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);  // the forward's bits
+                const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
+                float G0 = fast_expf(pw0), G1 = fast_expf(pw1);
+                settle_threshold2(pw0, co0.w, G0, pw1, co1.w, G1);
                 float wv0, qv0, wv1, qv1;
-                step(j0, hi - 1 - j0, true, rec0(j0), pos(j0), wv0, qv0);
-                step(j1, hi - 1 - j1, has1, rec0(j1), pos(j1), wv1, qv1);
-#endif
+                step(j0, hi - 1 - j0, true, co0.w, pw0, G0, wv0, qv0);
+                step(j1, hi - 1 - j1, has1, co1.w, pw1, G1, wv1, qv1);
                 float* wr = wq + r * WQS + l;
                 wr[0] = wv0;
                 wr[GRP * WQS] = qv0;
@@ -573,11 +550,6 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
                     flush(r);
                     r = 0;
                 }
-#if R3DG_BWD_PF
-                cur = nxt;
-                j0 = n0; j1 = n1; has1 = nh1;
-                co0 = nco0; co1 = nco1; xy0 = nxy0; xy1 = nxy1;
-#endif
             }
         }
     }
@@ -1002,26 +974,36 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
 }
 
 template <int SMAX>
-static hipError_t launch_gather_s(const GatherBwdArgs& a, hipStream_t stream) {
+static hipError_t launch_gather_s(const GatherBwdArgs& a, bool row_sum, hipStream_t stream) {
     constexpr int NXC = 4 * ((4 + SMAX + 15) / 16);
     constexpr int LPG = NXC + 2 <= 8 ? 8 : 16;
     const int n = a.g_end - a.g_begin;
     if (n <= 0) return hipSuccess;
-    const long long threads = (long long)n * LPG;
-    hipLaunchKernelGGL((row_sum_kernel<SMAX>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL((gather_bwd_kernel<SMAX>), dim3((n + 255) / 256), dim3(256), 0, stream, a);
+    if (row_sum) {
+        const long long threads = (long long)n * LPG;
+        hipLaunchKernelGGL((row_sum_kernel<SMAX>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
+    } else {
+        hipLaunchKernelGGL((gather_bwd_kernel<SMAX>), dim3((n + 255) / 256), dim3(256), 0, stream, a);
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_gather_backward(const GatherBwdArgs& a, hipStream_t stream) {
+static hipError_t launch_per_gaussian(const GatherBwdArgs& a, bool row_sum, hipStream_t stream) {
     if (a.P == 0) return hipSuccess;
-    if (a.S == 0) return launch_gather_s<0>(a, stream);
-    if (a.S <= 4) return launch_gather_s<4>(a, stream);
-    if (a.S <= 8) return launch_gather_s<8>(a, stream);
-    if (a.S <= 12) return launch_gather_s<12>(a, stream);
-    if (a.S <= 16) return launch_gather_s<16>(a, stream);
-    if (a.S <= 24) return launch_gather_s<24>(a, stream);
-    return launch_gather_s<32>(a, stream);
+    if (a.S == 0) return launch_gather_s<0>(a, row_sum, stream);
+    if (a.S <= 4) return launch_gather_s<4>(a, row_sum, stream);
+    if (a.S <= 8) return launch_gather_s<8>(a, row_sum, stream);
+    if (a.S <= 12) return launch_gather_s<12>(a, row_sum, stream);
+    if (a.S <= 16) return launch_gather_s<16>(a, row_sum, stream);
+    if (a.S <= 24) return launch_gather_s<24>(a, row_sum, stream);
+    return launch_gather_s<32>(a, row_sum, stream);
+}
+
+// the per-instance gradient reduction of renderCUDA's backward (row_sum_kernel)
+hipError_t launch_row_sum(const GatherBwdArgs& a, hipStream_t stream) { return launch_per_gaussian(a, true, stream); }
+// computeCov2DCUDA + preprocessCUDA backward (gather_bwd_kernel), after launch_row_sum
+hipError_t launch_gather_backward(const GatherBwdArgs& a, hipStream_t stream) {
+    return launch_per_gaussian(a, false, stream);
 }
 
 }  // namespace r3dg

@@ -34,8 +34,8 @@ R3DG_EXP_READER(r3dg_exp_counters_fwd)
 #ifndef R3DG_FWD_PRED
 #define R3DG_FWD_PRED 0  // 1: accumulation predicated (weight 0) instead of branched (measured slower)
 #endif
-#ifndef R3DG_FWD_HOIST
-#define R3DG_FWD_HOIST 0  // 1: both paired instances' conic / position read up front (measured: no gain)
+#ifndef R3DG_FWD_PKEXP
+#define R3DG_FWD_PKEXP 1  // 1: a pair's two exps as packed f32 ops (bit-identical per component)
 #endif
 #ifndef R3DG_FWD_PAIR
 #define R3DG_FWD_PAIR 1  // two compacted instances per loop iteration
@@ -86,7 +86,7 @@ render_fwd_kernel(RenderFwdArgs a) {
                 const float4 co = rec[0], r1 = rec[1];
                 const float2 xy = make_float2(r1.x, r1.y);
                 s_xy[t] = xy;
-                s_co[t] = exp2_conic(co);
+                s_co[t] = co;
                 m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
 #pragma unroll
                 for (int q = 0; q < NA4; ++q) s_attr[q * NB + t] = rec[2 + q];
@@ -94,7 +94,7 @@ render_fwd_kernel(RenderFwdArgs a) {
                 const float2 xy = a.means2D[gid];
                 const float4 co = a.conic_opacity[gid];
                 s_xy[t] = xy;
-                s_co[t] = exp2_conic(co);
+                s_co[t] = co;
                 m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
                 float v[NA4 * 4];
 #pragma unroll
@@ -129,7 +129,8 @@ render_fwd_kernel(RenderFwdArgs a) {
         __syncthreads();
         // One blend step of renderCUDA (forward.cu:470-520): the tests are predicated, every LDS
         // read of the instance is issued before them, and only the accumulation is a branch.
-        auto step = [&](int j, bool live, float4 co, float2 xy) {
+        // `power` and G = r3dg_expf(power) come from the caller (a pair's two exps run packed).
+        auto step = [&](int j, bool live, float opacity, float power, float G) {
 #pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
             float v[NA4 * 4];
 #pragma unroll
@@ -137,8 +138,7 @@ render_fwd_kernel(RenderFwdArgs a) {
                 const float4 r = s_attr[q * NB + j];
                 v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
             }
-            const float power = gauss_power2(co, xy.x - pfx, xy.y - pfy);  // exp2-domain conic
-            const float alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(power));
+            const float alpha = fminf(0.99f, opacity * G);  // bit-identical to the oracle
             const bool contrib = live && !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
             const float test_T = T * (1.0f - alpha);
             const bool stop = test_T < 0.0001f;
@@ -198,22 +198,31 @@ render_fwd_kernel(RenderFwdArgs a) {
                 const bool has1 = bits != 0u;
                 const int j1 = has1 ? c * 32 + __builtin_ctz(bits) : j0;
                 bits &= bits - 1;
-#if R3DG_FWD_HOIST
-                // both instances' conic / position read before the first step's tests: the second
-                // step's reads no longer wait behind the first step's accumulation branch
-                const float4 co0 = s_co[j0], co1 = s_co[j1];
-                const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
-                step(j0, true, co0, xy0);
-                step(j1, has1, co1, xy1);
+                {
+                    // both exps at once (packed): neither depends on T
+                    const float4 co0 = s_co[j0], co1 = s_co[j1];
+                    const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
+                    const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
+                    const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
+#if R3DG_FWD_PKEXP
+                    const f32x2 G = r3dg_expf2(pw0, pw1);
+                    step(j0, true, co0.w, pw0, G.x);
+                    step(j1, has1, co1.w, pw1, G.y);
 #else
-                step(j0, true, s_co[j0], s_xy[j0]);
-                step(j1, has1, s_co[j1], s_xy[j1]);
+                    step(j0, true, co0.w, pw0, r3dg_expf(pw0));
+                    step(j1, has1, co1.w, pw1, r3dg_expf(pw1));
 #endif
+                }
                 if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
 #else
                 const int j0 = c * 32 + __builtin_ctz(bits);
                 bits &= bits - 1;
-                step(j0, true, s_co[j0], s_xy[j0]);
+                {
+                    const float4 co0 = s_co[j0];
+                    const float2 xy0 = s_xy[j0];
+                    const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
+                    step(j0, true, co0.w, pw0, r3dg_expf(pw0));
+                }
 #endif
                 if (__ballot(!done) == 0ull) {  // converged here: a uniform exit
                     alive = false;
@@ -306,7 +315,7 @@ __global__ void __launch_bounds__(kBlock) intermediate_kernel(IntermediateArgs a
             const float dx = xy.x - (float)px, dy = xy.y - (float)py;
             const float power = gauss_power(co, dx, dy);
             if (power > 0.0f) continue;
-            const float G = __expf(power);
+            const float G = r3dg_expf(power);
             const float alpha = fminf(0.99f, co.w * G);
             const float salpha = fminf(0.99f, s_so[j] * G);
             if (alpha < 1.0f / 255.0f && salpha < 1.0f / 255.0f) continue;
