@@ -11,11 +11,14 @@ parallelism, every rank renders its own camera of the same scene (weak scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Rank 0 prints one JSON line. `roofline` prices the tile-blend kernels (render fwd + render bwd)
-with SURVEY.md §8d's algorithmic bytes (272*L + 156*H*W + 16*tiles at S=11) over their HIP-event
-device time measured on the launch stream during the timed steps; `traffic` is the HBM bytes of
-the same two kernels from rocprofv3 PMC counters (profiles/, FETCH_SIZE doubled per
-MI355X_MICROARCH.md §HBM), or null. `cpu_baseline` times the CPU oracle (a scalar C port of the
+Rank 0 prints one JSON line. `roofline` prices renderCUDA fwd + bwd -- render_fwd_kernel,
+render_bwd_mfma_kernel and row_sum_kernel (the backward's per-instance reduction) -- with SURVEY.md
+§8d's algorithmic bytes (272*L + 156*H*W + 16*tiles at S=11) over their device time, from HIP
+events recorded inside each launch's dispatch on the launch stream during the timed steps;
+`traffic` is the HBM bytes of the same kernels from rocprofv3 PMC counters (profiles/, FETCH_SIZE
+doubled per MI355X_MICROARCH.md §HBM), or null; `roofline.valu` is the compute side: VALU
+lane-instructions per second (PMC SQ_INSTS_VALU per launch, profiles/valu_latest.json) over the same
+live launch times against the VALU issue peak, with the evaluated pixel x instance pairs. `cpu_baseline` times the CPU oracle (a scalar C port of the
 reference path) on a bounded sample of the same workload.
 """
 from __future__ import annotations
@@ -51,7 +54,9 @@ def load_traffic() -> dict | None:
         return json.load(f)
 
 
-VALU_PEAK = 256 * 4 * 16 * 2.4e9  # lane-instructions/s: 256 CUs x 4 SIMD16 x 2.4 GHz (one wave64 op = 4 cycles)
+# VALU issue peak, lane-instructions/s: 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz
+# (MI355X_MICROARCH.md: a wave64 VALU op issues over 2 cycles; = the 157.3 TFLOP/s f32 vector peak / 2)
+VALU_PEAK = 256 * 4 * 32 * 2.4e9
 
 
 def load_valu(P: int) -> dict | None:

@@ -457,17 +457,19 @@ def bvh_build(leaf_aabbs):
     return nodes, aabbs, keys
 
 
-def bvh_trace_opacity(nodes, aabbs, rays_o, rays_d, means3D, cov_inv, opacity, normals):
-    """trace_bvh_opacity -> (contribute int32 [R], visibility f32 [R], transmittance before the cut [R])."""
+def bvh_trace_opacity(nodes, aabbs, rays_o, rays_d, means3D, cov_inv, opacity, normals, with_terms=False):
+    """trace_bvh_opacity -> (contribute int32 [R], visibility f32 [R], transmittance before the cut [R]
+    [, factors multiplied into it int32 [R] when with_terms])."""
     o, d = _f(rays_o).reshape(-1, 3), _f(rays_d).reshape(-1, 3)
     R = o.shape[0]
     contrib = np.zeros(R, np.int32)
     vis = np.ones(R, F)
     t_last = np.ones(R, F)
+    nterms = np.zeros(R, np.int32)
     lib().oracle_bvh_trace_opacity(ctypes.c_int(R), _p(np.ascontiguousarray(nodes, np.int32)), _p(_f(aabbs)), _p(o),
                                    _p(d), _p(_f(means3D)), _p(_f(cov_inv)), _p(_f(opacity).reshape(-1)),
-                                   _p(_f(normals)), _p(contrib), _p(vis), _p(t_last))
-    return contrib, vis, t_last
+                                   _p(_f(normals)), _p(contrib), _p(vis), _p(t_last), _p(nterms))
+    return (contrib, vis, t_last, nterms) if with_terms else (contrib, vis, t_last)
 
 
 def bvh_trace(nodes, aabbs, rays_o, rays_d, means3D):

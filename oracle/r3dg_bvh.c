@@ -259,7 +259,7 @@ static int push_children(const int32_t* nodes, const float* aabbs, int node, con
  * cut), so tests can tell rays that sit on the threshold */
 void oracle_bvh_trace_opacity(int R, const int32_t* nodes, const float* aabbs, const float* rays_o,
                               const float* rays_d, const float* means, const float* cov, const float* opac,
-                              const float* normals, int32_t* contrib, float* vis, float* t_last) {
+                              const float* normals, int32_t* contrib, float* vis, float* t_last, int32_t* nterms) {
     for (int ray = 0; ray < R; ++ray) {
         const float* o = rays_o + 3 * (long)ray;
         const float* d = rays_d + 3 * (long)ray;
@@ -301,6 +301,7 @@ void oracle_bvh_trace_opacity(int R, const int32_t* nodes, const float* aabbs, c
             }
         }
         if (t_last) t_last[ray] = T;
+        if (nterms) nterms[ray] = count; /* factors multiplied into T, up to and including the cut */
         contrib[ray] = done ? 0 : count;
         vis[ray] = done ? 0.f : T;
     }

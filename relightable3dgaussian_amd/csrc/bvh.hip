@@ -422,7 +422,17 @@ __global__ void __launch_bounds__(256) bvh_ray_morton_kernel(int R, const float*
 #define R3DG_BVH_LDS 16  // measured: 8 / 12 / 16 / 24 / 32 entries (tools/exp_bvh.sh); 16 fills 7 waves per SIMD
 #endif
 constexpr int kLdsStack = R3DG_BVH_LDS;  // per-lane stack entries in LDS ([entry][lane]: conflict-free)
-constexpr float kLogCut = -0.10536052f - 1e-5f;  // log(0.9) minus a rounding margin
+// Group cut in the log domain. Every term a lane adds is __logf(1 - alpha) + kLogSlack, where
+// kLogSlack bounds, per term, everything that separates the running sum from log of the
+// reference's single-chain product: v_log_f32 (<= 1 ulp of a log2 in [-0.152, 0]: 1.5e-8), the ln 2
+// scaling (4e-9), the LDS sum's rounding (|sum| < 0.2: 7.5e-9) and the reference chain's own
+// f32 multiply per factor (2^-24 relative: 6e-8) -- 8.7e-8 in all, taken as 2e-7. A factor below
+// 0.9 never reaches the sum (its lane's own product cuts exactly first). So a sum below
+// log(0.9) - 1e-7 proves the reference's transmittance fell below 0.9: the ray is occluded
+// whatever the remaining terms, and only then does the group stop early. Rays that never prove
+// it finish, and the group's exact product decides.
+constexpr float kLogCut = -0.10536052f - 1e-7f;
+constexpr float kLogSlack = 2e-7f;
 
 // trace_bvh_opacity_cuda (trace.cu:199-286): transmittance along the ray through every Gaussian
 // whose box it crosses (front-facing normals, opacity >= 1/255, density maximum at t >= 0.01);
@@ -484,9 +494,7 @@ __global__ void __launch_bounds__(256) bvh_trace_opacity_kernel(TraceOpacityArgs
     float T = 1.f;
     bool occluded = false;
     while (sp > 0) {
-        // the group's running transmittance (log domain, LDS atomics) crossed the cut: stop. The
-        // 1e-5 margin keeps __logf rounding from cutting a ray whose exact product is >= 0.9;
-        // rays inside the margin finish their traversal and the exact product decides
+        // the group's certified log-domain sum crossed the cut (kLogCut): occluded, stop
         if (gb > 0 && *(volatile float*)&lsum[gid] < kLogCut) break;
         --sp;
         const int rf = sp < kLdsStack ? lstack[sp][tid] : ostack[sp - kLdsStack];
@@ -510,7 +518,7 @@ __global__ void __launch_bounds__(256) bvh_trace_opacity_kernel(TraceOpacityArgs
                 if (gb > 0) lsum[gid] = -INFINITY;
                 break;
             }
-            if (gb > 0) atomicAdd(&lsum[gid], __logf(1 - alpha));
+            if (gb > 0) atomicAdd(&lsum[gid], __logf(1 - alpha) + kLogSlack);
         } else {
             const float4* r = a.nrec + 4 * (size_t)rf;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
@@ -629,7 +637,7 @@ __global__ void __launch_bounds__(256) bvh_trace_opacity_shared_kernel(TraceOpac
                             occluded = true;
                             lsum[gid] = -INFINITY;
                         } else {
-                            atomicAdd(&lsum[gid], __logf(1 - alpha));
+                            atomicAdd(&lsum[gid], __logf(1 - alpha) + kLogSlack);
                         }
                     }
                 }

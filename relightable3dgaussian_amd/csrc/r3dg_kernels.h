@@ -2,6 +2,8 @@
 // translation units and the host orchestration (rasterizer.hip).
 #pragma once
 
+#include <hip/hip_ext.h>
+
 #include "r3dg_common.h"
 
 namespace r3dg {
@@ -54,6 +56,7 @@ struct RenderFwdArgs {
     float* out_depth;
     float* out_feature;
     float* out_shader_color;
+    float* zero_stencil;  // stencil output to zero (default splat shaders), or null
     FeatureLayout flay;
 };
 
@@ -227,5 +230,24 @@ static __device__ unsigned long long g_exp_cnt[8];  // one copy per translation 
 #else
 #define R3DG_EXP_ADD(i, v) ((void)0)
 #endif
+
+// ---- profiled launches ----------------------------------------------------------------------
+// While r3dg_profile_enable is active, a profiled stage (rasterizer.hip ProfScope) hands its
+// start / stop events to the stage's kernel launch, which records them as part of the dispatch
+// (hipExtLaunchKernelGGL): device-side timestamps with no separate marker packets between
+// kernels, so profiling does not add gaps to the timed steps.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents take_launch_events();  // the pending pair (cleared), or nulls when none is pending
+
+template <typename K, typename... Args>
+inline void launch_kernel(K kernel, dim3 grid, dim3 block, hipStream_t stream, Args... args) {
+    const LaunchEvents e = take_launch_events();
+    if (e.start)
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, stream, e.start, e.stop, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, stream, args...);
+}
 
 }  // namespace r3dg

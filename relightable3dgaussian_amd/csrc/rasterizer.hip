@@ -184,20 +184,69 @@ struct Profiler {
 static Profiler g_prof;
 static std::mutex g_prof_mu;
 
+static thread_local LaunchEvents t_pending;
+LaunchEvents take_launch_events() {
+    const LaunchEvents e = t_pending;
+    t_pending = LaunchEvents{};
+    return e;
+}
+
+// A profiled stage. Kernel stages (the default) pass the events to their launch (launch_kernel,
+// r3dg_kernels.h): timestamps inside the dispatch packet, no marker packets between kernels.
+// Marker stages (library calls such as the rocPRIM sorts) record the events around the calls;
+// they are recorded only when R3DG_PROF_SORT is set, since marker packets add gaps to the stream.
 struct ProfScope {
     int k;
     hipStream_t st;
+    bool marker;
     int idx = -1;
-    ProfScope(int kind, hipStream_t s) : k(kind), st(s) {
+    ProfScope(int kind, hipStream_t s, bool markers = false) : k(kind), st(s), marker(markers) {
+        static const bool sort_markers = getenv("R3DG_PROF_SORT") != nullptr;
+        if (marker && !sort_markers) return;
         if (g_prof.max_records > 0 && g_prof.n[k] < g_prof.max_records) {
             idx = g_prof.n[k]++;
-            (void)hipEventRecord(g_prof.ev[k][0][idx], st);
+            if (marker) (void)hipEventRecord(g_prof.ev[k][0][idx], st);
+            else t_pending = LaunchEvents{g_prof.ev[k][0][idx], g_prof.ev[k][1][idx]};
         }
     }
     ~ProfScope() {
-        if (idx >= 0) (void)hipEventRecord(g_prof.ev[k][1][idx], st);
+        if (idx < 0) return;
+        if (marker) {
+            (void)hipEventRecord(g_prof.ev[k][1][idx], st);
+        } else if (t_pending.start) {  // no launch took the events (empty stage): zero duration
+            (void)hipEventRecord(t_pending.start, st);
+            (void)hipEventRecord(t_pending.stop, st);
+            t_pending = LaunchEvents{};
+        }
     }
 };
+
+// Pinned host word + event for the num_rendered readback, one per (host thread, device): a
+// thread's calls on one device are issued in order, so the slot is free again by its next call.
+struct Readback {
+    uint32_t* host = nullptr;
+    hipEvent_t ev = nullptr;
+};
+static hipError_t readback_slot(Readback** out) {
+    constexpr int kMaxDevices = 64;
+    thread_local Readback slots[kMaxDevices];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    Readback& r = slots[dev];
+    if (!r.host) {
+        void* p = nullptr;
+        if ((e = hipHostMalloc(&p, 64, hipHostMallocDefault)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&r.ev, hipEventDisableTiming)) != hipSuccess) {
+            (void)hipHostFree(p);
+            return e;
+        }
+        r.host = static_cast<uint32_t*>(p);
+    }
+    *out = &r;
+    return hipSuccess;
+}
 
 // rasterizer_impl.cu:37-52
 static uint32_t higher_msb(uint32_t n) {
@@ -532,17 +581,25 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         pa.rgb = geom.rgb; pa.clamped = geom.clamped; pa.error_flag = nullptr;
         {
             ProfScope ps(R3DG_PROF_PREPROCESS, st);
-            hipLaunchKernelGGL(preprocess_kernel, dim3((P + 255) / 256), dim3(256), 0, st, pa);
+            launch_kernel(preprocess_kernel, dim3((P + 255) / 256), dim3(256), st, pa);
         }
         R3DG_CHECK_LAUNCH(s->debug, st);
 
         size_t tb = geom.scan_temp_bytes;
         R3DG_CHECK_HIP(rocprim::inclusive_scan(geom.scan_temp, tb, geom.tiles_touched, geom.point_offsets,
                                                (size_t)P, rocprim::plus<uint32_t>(), st));
+        // num_rendered (rasterizer_impl.cu:259-263 reads it with a blocking cudaMemcpy): copied into
+        // pinned host memory right after the scan; the host then waits on an event behind that copy
+        // only, so its wake-up overlaps the depth sort enqueued below instead of idling the GPU
+        Readback* rb = nullptr;
+        R3DG_CHECK_HIP(readback_slot(&rb));
+        R3DG_CHECK_HIP(hipMemcpyAsync(rb->host, geom.point_offsets + P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                      st));
+        R3DG_CHECK_HIP(hipEventRecord(rb->ev, st));
         {
             // Gaussians by ascending depth bits, stable (ties keep ascending id), then the
             // instance offsets in that order; both overlap the host read of num_rendered below
-            ProfScope ps(R3DG_PROF_SORT, st);
+            ProfScope ps(R3DG_PROF_SORT, st, true);
             size_t db = geom.depth_sort_temp_bytes;
             R3DG_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(geom.depth_sort_temp, db, geom.depth_keys,
                                                      geom.depth_keys_sorted, rocprim::counting_iterator<uint32_t>(0),
@@ -552,9 +609,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
                                                    depth_order_touched(geom.tiles_touched, geom.depth_order),
                                                    geom.depth_scan, (size_t)P, rocprim::plus<uint32_t>(), st));
         }
-        uint32_t Lh = 0;
-        R3DG_CHECK_HIP(hipMemcpyAsync(&Lh, geom.point_offsets + P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        R3DG_CHECK_HIP(hipStreamSynchronize(st));
+        R3DG_CHECK_HIP(hipEventSynchronize(rb->ev));
+        const uint32_t Lh = *rb->host;
         R3DG_REQUIRE(Lh < (1u << 31), "rasterize_gaussians: too many tile instances");
         L = (int)Lh;
     }
@@ -576,7 +632,7 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         const int bit = (int)higher_msb((uint32_t)T);
         size_t sb = bin.sort_temp_bytes;
         {
-            ProfScope ps(R3DG_PROF_SORT, st);
+            ProfScope ps(R3DG_PROF_SORT, st, true);
             R3DG_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(bin.sort_temp, sb, bin.tile_keys, bin.tile_sorted,
                                                                  bin.gid_in, bin.point_list, (size_t)L, 0, bit, st));
         }
@@ -618,9 +674,6 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         hipLaunchKernelGGL(refresh_record_opacity_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, radii,
                            geom.conic_opacity, geom.records, record_f4(S));
         R3DG_CHECK_LAUNCH(s->debug, st);
-    } else if (out->stencil) {
-        // default splat shaders leave every stencil value 0 (InitializeStencil, rasterizer_impl.cu:203-209)
-        R3DG_CHECK_HIP(hipMemsetAsync(out->stencil, 0, sizeof(float) * (size_t)H * W, st));
     }
 
     RenderFwdArgs ra{};
@@ -645,6 +698,9 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     ra.out_feature = out->feature;
     ra.out_shader_color = out->shader_color;
     ra.flay = make_feature_layout(S, (long long)H * W, true);
+    // default splat shaders leave every stencil value 0 (InitializeStencil, rasterizer_impl.cu:203-209):
+    // the blend writes those zeros with its other outputs (no separate memset launch)
+    ra.zero_stencil = splat_active ? nullptr : out->stencil;
     if (const char* e = getenv("R3DG_NO_CULL")) ra.cull = (e[0] == '0');
     {
         ProfScope ps(R3DG_PROF_RENDER_FWD, st);

@@ -569,11 +569,11 @@ static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
     const char* e = getenv("R3DG_BWD");
     const int grid = padded_tile_grid(a.num_tiles);
     if (e && e[0] == 'd')
-        hipLaunchKernelGGL((render_bwd_dpp_kernel<SMAX>), dim3(grid), dim3(kBlock), 0, stream, a);
+        launch_kernel(render_bwd_dpp_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
     else if (e && e[0] == 'w')
-        hipLaunchKernelGGL((render_bwd_mfma_kernel<SMAX, true>), dim3(4 * grid), dim3(64), 0, stream, a);
+        launch_kernel(render_bwd_mfma_kernel<SMAX, true>, dim3(4 * grid), dim3(64), stream, a);
     else
-        hipLaunchKernelGGL((render_bwd_mfma_kernel<SMAX, false>), dim3(grid), dim3(kBlock), 0, stream, a);
+        launch_kernel(render_bwd_mfma_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
     return hipGetLastError();
 }
 
@@ -981,9 +981,9 @@ static hipError_t launch_gather_s(const GatherBwdArgs& a, bool row_sum, hipStrea
     if (n <= 0) return hipSuccess;
     if (row_sum) {
         const long long threads = (long long)n * LPG;
-        hipLaunchKernelGGL((row_sum_kernel<SMAX>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, a);
+        launch_kernel(row_sum_kernel<SMAX>, dim3((unsigned)((threads + 255) / 256)), dim3(256), stream, a);
     } else {
-        hipLaunchKernelGGL((gather_bwd_kernel<SMAX>), dim3((n + 255) / 256), dim3(256), 0, stream, a);
+        launch_kernel(gather_bwd_kernel<SMAX>, dim3((n + 255) / 256), dim3(256), stream, a);
     }
     return hipGetLastError();
 }

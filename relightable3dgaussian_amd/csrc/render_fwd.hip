@@ -252,6 +252,7 @@ render_fwd_kernel(RenderFwdArgs a) {
         }
         a.out_depth[pix] = Dp;
         a.out_opacity[pix] = Op;
+        if (a.zero_stencil) a.zero_stencil[pix] = 0.f;
 #pragma unroll
         for (int c = 0; c < SMAX; ++c)
             if (c < a.S) a.out_feature[a.flay.a[c] + pix * a.flay.m[c]] = F[c];
@@ -262,9 +263,9 @@ template <int SMAX>
 static hipError_t launch_fwd_s(const RenderFwdArgs& a, bool shader, hipStream_t stream) {
     const int grid = padded_tile_grid(a.num_tiles);
     if (shader)
-        hipLaunchKernelGGL((render_fwd_kernel<SMAX, true>), dim3(grid), dim3(kBlock), 0, stream, a);
+        launch_kernel(render_fwd_kernel<SMAX, true>, dim3(grid), dim3(kBlock), stream, a);
     else
-        hipLaunchKernelGGL((render_fwd_kernel<SMAX, false>), dim3(grid), dim3(kBlock), 0, stream, a);
+        launch_kernel(render_fwd_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
     return hipGetLastError();
 }
 

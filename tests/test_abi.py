@@ -128,14 +128,20 @@ def test_alias_makes_reference_import_work():
     assert r3dg_rasterization._C is r._C
 
 
+# gaussian_renderer/r3dg_rasterization.py:198-222, the NamedTuple's 24 fields in order
+REFERENCE_SETTINGS_FIELDS = (
+    "image_height", "image_width", "tanfovx", "tanfovy", "cx", "cy", "bg", "scale_modifier", "viewmatrix",
+    "viewmatrix_inv", "projmatrix", "projmatrix_inv", "sh_degree", "campos", "prefiltered", "backward_geometry",
+    "computer_pseudo_normal", "debug", "h_shShaderManager_ptr", "h_splatShaderManager_ptr", "time", "dt",
+    "d_textureManager_ptr", "postProcessingPasses")
+
+
 def test_settings_fields_match_reference():
-    """GaussianRasterizationSettings field order (r3dg_rasterization/__init__.py NamedTuple)."""
+    """GaussianRasterizationSettings: the reference's 24 fields, same names, same order (neilf.py
+    constructs it by keyword, _RasterizeGaussians reads it by attribute)."""
     from relightable3dgaussian_amd.r3dg_rasterization import GaussianRasterizationSettings
 
-    assert GaussianRasterizationSettings._fields[:6] == ("image_height", "image_width", "tanfovx", "tanfovy", "cx",
-                                                         "cy")
-    assert "backward_geometry" in GaussianRasterizationSettings._fields
-    assert "computer_pseudo_normal" in GaussianRasterizationSettings._fields
+    assert GaussianRasterizationSettings._fields == REFERENCE_SETTINGS_FIELDS
 
 
 def test_no_cpu_fallback():
