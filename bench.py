@@ -14,7 +14,8 @@ parallelism, every rank renders its own camera of the same scene (weak scaling).
 Rank 0 prints one JSON line. `roofline` prices renderCUDA fwd + bwd -- render_fwd_kernel,
 render_bwd_mfma_kernel and row_sum_kernel (the backward's per-instance reduction) -- with SURVEY.md
 §8d's algorithmic bytes (272*L + 156*H*W + 16*tiles at S=11) over their device time, from HIP
-events recorded inside each launch's dispatch on the launch stream during the timed steps;
+events recorded inside each launch's dispatch on the launch stream during K further steps (the
+timed K steps run without events);
 `traffic` is the HBM bytes of the same kernels from rocprofv3 PMC counters (profiles/, FETCH_SIZE
 doubled per MI355X_MICROARCH.md §HBM), or null; `roofline.valu` is the compute side: VALU
 lane-instructions per second (PMC SQ_INSTS_VALU per launch, profiles/valu_latest.json) over the same
@@ -296,7 +297,6 @@ def main() -> None:
     for _ in range(args.warmup):
         L = step()
     torch.cuda.synchronize()
-    _C.profile_enable(args.steps + 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -307,6 +307,12 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # per-kernel device times: K more steps with HIP events inside the profiled launches (kept out
+    # of the timed region above)
+    _C.profile_enable(args.steps + 1)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
     prof = {k: _C.profile_read(i) for i, k in enumerate(["render_fwd", "render_bwd", "gather_bwd", "sort",
                                                           "preprocess", "row_sum"])}
     _C.profile_enable(0)
@@ -323,7 +329,7 @@ def main() -> None:
     value = world * npix * args.steps / elapsed / 1e6
     tiles = ((W + 15) // 16) * ((H + 15) // 16)
     bf, bb = algorithmic_bytes(L, npix, tiles, S_M1)
-    # per-step device time of each stage (sort = depth sort + tile sort: two scopes per step)
+    # per-step device time of each stage
     avg = {k: v[1] / args.steps for k, v in prof.items()}
     launch = {k: (v[1] / v[0] if v[0] else float("nan")) for k, v in prof.items()}
     # renderCUDA fwd + bwd: the backward blend AND its per-instance reduction (row_sum_kernel sums
@@ -358,7 +364,7 @@ def main() -> None:
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "renderCUDA fwd + bwd: render_fwd_kernel + render_bwd_mfma_kernel + row_sum_kernel",
                      "algorithmic_bytes": bf + bb, "kernel_ms": round(t_kern * 1e3, 4), "valu": valu},
-        "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+        "kernel_ms": {k: round(v, 4) for k, v in avg.items() if prof[k][0]},
     }
     if world == 1:
         res["bvh_visibility"] = bvh_visibility(means3D, scales, rots, dev)

@@ -7,6 +7,8 @@
 // the keys and the sort order are reproducible (SURVEY.md §7 "Bit-exact keys").
 #pragma clang fp contract(off)
 
+#include <rocprim/block/block_radix_sort.hpp>
+
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
 
@@ -207,37 +209,35 @@ __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* _
     present[idx] = xform_point4x3(p, view).z <= 0.2f ? 0 : 1;
 }
 
-// rasterizer_impl.cu:72-113 (duplicateWithKeys). The value sorted alongside each key is its
-// unsorted slot, so the sort permutation can route backward contributions to Gaussian-
-// contiguous rows; gid_of_slot maps a slot back to its Gaussian.
-// duplicateWithKeys (rasterizer_impl.cu:72-113) in depth order. Block b expands the Gaussians of
-// depth ranks [256b, 256b+256) (ascending depth bits, ties by ascending id) into their tiles,
-// row-major over each rect as the reference. Their instances occupy one contiguous range of the
-// depth-ordered list, so the block writes it cooperatively (coalesced): output position q finds
-// its Gaussian by binary search over the block's instance offsets. A stable sort of this list by
-// tile reproduces the reference's stable sort by (tile << 32 | depth bits) with a 13-bit key.
-__global__ void __launch_bounds__(256) duplicate_in_depth_order_kernel(
-    int P, const uint32_t* __restrict__ order, const uint32_t* __restrict__ depth_scan,
-    const float2* __restrict__ means2D, const int* __restrict__ radii, int grid_x, int grid_y,
-    uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ gid_out, const uint32_t* __restrict__ offsets,
-    float4* __restrict__ records, int rec4) {
+// duplicateWithKeys (rasterizer_impl.cu:72-113). Block b expands the Gaussians [256b, 256b+256)
+// into their tiles, row-major over each rect as the reference, at their Gaussian-major slots
+// offsets[g-1] + k: the block's instances are one contiguous slot range, written cooperatively
+// (coalesced; output position q finds its Gaussian by binary search over the block's instance
+// offsets). The key is the tile alone: a stable sort by tile keeps each tile's instances in
+// ascending Gaussian order, and tile_depth_sort_kernel then orders every tile by depth, stably --
+// together the reference's stable sort by (tile << 32 | depth bits) over the Gaussian-major list.
+// The four backward row flags of each slot (render_bwd.hip) are zeroed on the way.
+__global__ void __launch_bounds__(256) duplicate_kernel(int P, const uint32_t* __restrict__ offsets,
+                                                        const float2* __restrict__ means2D,
+                                                        const int* __restrict__ radii, int grid_x, int grid_y,
+                                                        uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ gid_out,
+                                                        uint32_t* __restrict__ flags, float4* __restrict__ records,
+                                                        int rec4) {
     __shared__ uint32_t s_end[256];  // inclusive end of each Gaussian's instances, block-relative
-    __shared__ uint32_t s_gid[256];
     __shared__ int s_x0[256], s_y0[256], s_w[256];
     const int t = threadIdx.x;
     const int i0 = blockIdx.x * 256;
     const int n = min(256, P - i0);
-    const uint32_t base = i0 == 0 ? 0u : depth_scan[i0 - 1];
+    const uint32_t base = i0 == 0 ? 0u : offsets[i0 - 1];
     if (t < n) {
-        const uint32_t g = order[i0 + t];
-        s_end[t] = depth_scan[i0 + t] - base;
-        s_gid[t] = g;
+        const int g = i0 + t;
+        s_end[t] = offsets[g] - base;
         const int r = radii[g];
         int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
         if (r > 0) {
             const float2 m = means2D[g];
             get_rect(m.x, m.y, r, grid_x, grid_y, x0, y0, x1, y1);
-            if (records)  // the Gaussian's first unsorted slot, for the backward's rows
+            if (records)  // the Gaussian's first slot, for the backward's rows
                 reinterpret_cast<float*>(records + (size_t)g * rec4 + 1)[2] =
                     __uint_as_float(g == 0 ? 0u : offsets[g - 1]);
         }
@@ -258,55 +258,156 @@ __global__ void __launch_bounds__(256) duplicate_in_depth_order_kernel(
         const int w = s_w[lo];
         const int x = s_x0[lo] + (int)(k % (uint32_t)w), y = s_y0[lo] + (int)(k / (uint32_t)w);
         tile_keys[base + q] = (uint32_t)(y * grid_x + x);
-        gid_out[base + q] = s_gid[lo];
+        gid_out[base + q] = (uint32_t)(i0 + lo);
+        if (flags) flags[base + q] = 0u;
     }
 }
 
-// rasterizer_impl.cu:118-140 (identifyTileRanges)
-__global__ void __launch_bounds__(256) identify_ranges_kernel(int L, const uint32_t* __restrict__ tiles,
-                                                              uint2* __restrict__ ranges) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= L) return;
-    const uint32_t cur = tiles[idx];
-    if (idx == 0) {
-        ranges[cur].x = 0;
-    } else {
-        const uint32_t prev = tiles[idx - 1];
-        if (cur != prev) {
-            ranges[prev].y = idx;
-            ranges[cur].x = idx;
+// identifyTileRanges (rasterizer_impl.cu:118-140) as one binary search per tile over the sorted
+// tile ids: every tile's range is written (empty tiles (0, 0), the reference's memset value), so no
+// memset is needed.
+__global__ void __launch_bounds__(256) tile_ranges_kernel(int T, int L, const uint32_t* __restrict__ tiles,
+                                                          uint2* __restrict__ ranges) {
+    const int tile = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tile >= T) return;
+    auto lower = [&](uint32_t key) {
+        int lo = 0, hi = L;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (tiles[mid] < key) lo = mid + 1;
+            else hi = mid;
         }
-    }
-    if (idx == L - 1) ranges[cur].y = L;
+        return (uint32_t)lo;
+    };
+    const uint32_t b = lower((uint32_t)tile), e = lower((uint32_t)tile + 1u);
+    ranges[tile] = b < e ? make_uint2(b, e) : make_uint2(0u, 0u);  // empty: (0, 0) as the reference's memset
 }
 
-// Backward launch order, longest tiles first: one workgroup bucket-sorts the tiles by instance
-// count (bucket = count / 4, capped; descending). Only the schedule depends on this order (each
-// tile writes its own partial rows and the gather sums them in slot order), so the order within a
-// bucket, which LDS atomics leave unspecified, does not change any result.
+// Backward (and depth-sort) launch order, longest tiles first: one workgroup bucket-sorts the
+// tiles by instance count (bucket = count / 4, capped; descending). Only the schedule depends on
+// this order, so the order within a bucket, which LDS atomics leave unspecified, changes no result.
 __global__ void __launch_bounds__(1024) tile_order_kernel(int T, const uint2* __restrict__ ranges,
                                                           uint32_t* __restrict__ order) {
     constexpr int NBK = 1024;
     __shared__ uint32_t hist[NBK];
-    __shared__ uint32_t cursor[NBK];
+    __shared__ uint32_t scan[2][NBK];
     const int t = threadIdx.x;
     hist[t] = 0;
     __syncthreads();
     auto bucket = [&](int tile) {
-        const uint32_t c = ranges[tile].y - ranges[tile].x;
-        return (int)min(c >> 2, (uint32_t)(NBK - 1));
+        const uint2 r = ranges[tile];
+        return (int)min((r.y - r.x) >> 2, (uint32_t)(NBK - 1));
     };
     for (int i = t; i < T; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
     __syncthreads();
-    if (t == 0) {  // exclusive scan in descending bucket order
-        uint32_t run = 0;
-        for (int b = NBK - 1; b >= 0; --b) {
-            cursor[b] = run;
-            run += hist[b];
+    // exclusive scan in descending bucket order (Hillis-Steele over the reversed histogram)
+    const uint32_t v = hist[NBK - 1 - t];
+    int cur = 0;
+    scan[0][t] = v;
+    __syncthreads();
+    for (int o = 1; o < NBK; o <<= 1) {
+        const uint32_t x = scan[cur][t] + (t >= o ? scan[cur][t - o] : 0u);
+        scan[cur ^ 1][t] = x;
+        cur ^= 1;
+        __syncthreads();
+    }
+    hist[NBK - 1 - t] = scan[cur][t] - v;  // now the cursor of bucket NBK-1-t
+    __syncthreads();
+    for (int i = t; i < T; i += 1024) order[atomicAdd(&hist[bucket(i)], 1u)] = (uint32_t)i;
+}
+
+// The depth half of the reference's (tile << 32 | depth bits) sort: every tile's instances,
+// ascending Gaussian ids after the stable tile sort, sorted stably by the Gaussians' depth bits
+// (the reference's order: depth, ties by Gaussian id). One workgroup per tile, longest tiles
+// first. A tile of up to kSortChunk instances is sorted in registers / LDS (rocPRIM block radix
+// sort, 4 passes of 8 bits); a longer one sorts each chunk into a run and merges run pairs
+// (stable merge path) through the scratch buffers, ping-pong, landing in point_list.
+constexpr int kSortIPT = 4;
+constexpr int kSortChunk = 256 * kSortIPT;
+using TileDepthSort = rocprim::block_radix_sort<uint32_t, 256, kSortIPT, uint32_t>;
+
+__device__ __forceinline__ uint32_t nt_load(const uint32_t* p) { return __builtin_nontemporal_load(p); }
+
+__global__ void __launch_bounds__(256) tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges,
+                                                              const uint32_t* __restrict__ order,
+                                                              const uint32_t* __restrict__ depth_keys,
+                                                              uint32_t* __restrict__ point_list, uint32_t* kA,
+                                                              uint32_t* vA, uint32_t* kB) {
+    __shared__ typename TileDepthSort::storage_type storage;
+    const int b = blockIdx.x;
+    if (b >= T) return;
+    const int tile = order ? (int)order[b] : b;
+    const uint2 rg = ranges[tile];
+    const uint32_t s = rg.x, n = rg.y - rg.x;
+    if (n <= 1) return;
+    const int t = threadIdx.x;
+    const uint32_t nchunks = (n + kSortChunk - 1) / kSortChunk;
+    int rounds = 0;
+    while ((1u << rounds) < nchunks) ++rounds;
+    // runs go where an even number of merge rounds leaves the result in (kB, point_list)
+    uint32_t* rk = (rounds & 1) ? kA : kB;
+    uint32_t* rv = (rounds & 1) ? vA : point_list;
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        const uint32_t c0 = c * kSortChunk;
+        uint32_t keys[kSortIPT], vals[kSortIPT];
+#pragma unroll
+        for (int k = 0; k < kSortIPT; ++k) {  // blocked arrangement: item index = t * IPT + k
+            const uint32_t i = c0 + (uint32_t)(t * kSortIPT + k);
+            const uint32_t g = i < n ? point_list[s + i] : 0xffffffffu;
+            vals[k] = g;
+            keys[k] = i < n ? depth_keys[g] : 0xffffffffu;  // visible depths < 0x7f800000: pads sort last
+        }
+        if (c > 0) __syncthreads();  // storage reuse
+        TileDepthSort().sort(keys, vals, storage, 0, 32);
+#pragma unroll
+        for (int k = 0; k < kSortIPT; ++k) {
+            const uint32_t i = c0 + (uint32_t)(t * kSortIPT + k);
+            if (i < n) {
+                if (nchunks > 1) rk[s + i] = keys[k];
+                rv[s + i] = vals[k];
+            }
         }
     }
+    if (nchunks == 1) return;
     __syncthreads();
-    for (int i = t; i < T; i += 1024) order[atomicAdd(&cursor[bucket(i)], 1u)] = (uint32_t)i;
+    uint32_t *sk = rk, *sv = rv, *dk = (rk == kA) ? kB : kA, *dv = (rk == kA) ? point_list : vA;
+    for (uint32_t w = kSortChunk; w < n; w *= 2) {
+        for (uint32_t a0 = 0; a0 < n; a0 += 2 * w) {
+            const uint32_t a1 = min(a0 + w, n), b1 = min(a0 + 2 * w, n);
+            const uint32_t la = a1 - a0, lb = b1 - a1, tot = b1 - a0;
+            const uint32_t per = (tot + 255) / 256;
+            const uint32_t d0 = min((uint32_t)t * per, tot), d1 = min(d0 + per, tot);
+            if (d0 >= d1) continue;
+            const uint32_t* A = sk + s + a0;
+            const uint32_t* B = sk + s + a1;
+            // merge path: i = number of A items among the first d0 outputs (ties: A first)
+            uint32_t lo = d0 > lb ? d0 - lb : 0u, hi = min(d0, la);
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (nt_load(A + mid) <= nt_load(B + (d0 - 1 - mid))) lo = mid + 1;
+                else hi = mid;
+            }
+            uint32_t i = lo, j = d0 - lo;
+            uint32_t ka = i < la ? nt_load(A + i) : 0xffffffffu, kb = j < lb ? nt_load(B + j) : 0xffffffffu;
+            for (uint32_t d = d0; d < d1; ++d) {
+                const bool takeA = j >= lb || (i < la && ka <= kb);
+                if (takeA) {
+                    dk[s + a0 + d] = ka;
+                    dv[s + a0 + d] = nt_load(sv + s + a0 + i);
+                    ++i;
+                    ka = i < la ? nt_load(A + i) : 0xffffffffu;
+                } else {
+                    dk[s + a0 + d] = kb;
+                    dv[s + a0 + d] = nt_load(sv + s + a1 + j);
+                    ++j;
+                    kb = j < lb ? nt_load(B + j) : 0xffffffffu;
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t* tk = sk; sk = dk; dk = tk;
+        uint32_t* tv = sv; sv = dv; dv = tv;
+    }
 }
 
 }  // namespace r3dg

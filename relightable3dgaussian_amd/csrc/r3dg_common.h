@@ -57,34 +57,23 @@ struct GeomState {
     uint32_t* tiles_touched;// [P]
     uint32_t* point_offsets;// [P] inclusive scan of tiles_touched (Gaussian-contiguous slots)
     uint32_t* depth_keys;   // [P] depth bits (0xffffffff: not visible)
-    uint32_t* depth_keys_sorted; // [P]
-    uint32_t* depth_order;  // [P] Gaussian ids by ascending depth (stable)
-    uint32_t* depth_scan;   // [P] inclusive scan of tiles_touched in depth order
     void* scan_temp;
     size_t scan_temp_bytes;
-    void* depth_sort_temp;
-    size_t depth_sort_temp_bytes;
-    void* depth_scan_temp;
-    size_t depth_scan_temp_bytes;
     // [P, record_f4(S)] render records, last in the buffer (r3dg_kernels.h): only set when the
     // state is carved with S
     float4* records;
 };
 
-// tiles_touched of the i-th Gaussian in depth order (input of the depth-order scan)
-struct TouchedInDepthOrder {
-    const uint32_t* touched;
-    const uint32_t* order;
-    __host__ __device__ uint32_t operator()(uint32_t i) const { return touched[order[i]]; }
-};
 struct BinningState {
-    // Instances are generated in depth order (Gaussians sorted by depth bits), then stably sorted
-    // by tile: the result is the reference's stable sort by (tile << 32 | depth bits). The sort
-    // values are Gaussian ids, so the sorted values are the reference's point_list.
-    uint32_t* tile_keys;    // [L] tile of each instance, depth order (sort input)
+    // Instances are generated in the reference's Gaussian-major slot order, stably sorted by tile,
+    // then each tile stably by depth bits: the reference's stable sort by (tile << 32 | depth
+    // bits). The sort values are Gaussian ids, so the sorted values are the reference's point_list.
+    uint32_t* tile_keys;    // [L] tile of each instance, slot order (sort input; then depth-sort scratch)
     uint32_t* tile_sorted;  // [L] tile of each sorted instance
-    uint32_t* gid_in;       // [L] Gaussian of each depth-ordered instance (sort values)
+    uint32_t* gid_in;       // [L] Gaussian of each instance, slot order (sort values; then scratch)
     uint32_t* point_list;   // [L] Gaussian ids in sorted order (reference point_list)
+    uint32_t* keys2;        // [L] depth-sort scratch (tiles longer than one sort chunk)
+    uint32_t* flags;        // [L] backward row flags, one byte per (slot, quadrant) (render_bwd.hip)
     void* sort_temp;
     size_t sort_temp_bytes;
 };

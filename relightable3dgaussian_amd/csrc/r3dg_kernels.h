@@ -104,7 +104,6 @@ struct GatherBwdArgs {
     int P, D, M, S, RS, W, H, grid_x, grid_y;
     int g_begin, g_end;       // Gaussian range of this launch (outputs indexed by global id)
     const float* rows;        // partial rows (RenderBwdArgs)
-    const float* zero_row;    // RS zeros: the load target of quadrants without a row
     float* sums;              // [P, RS] per-Gaussian sums (row_sum_kernel -> gather_bwd_kernel)
     const uint32_t* flags;    // one word per slot: byte q set when quadrant q's row exists
     const float2* means2D;
@@ -160,11 +159,12 @@ struct IntermediateArgs {
 // kernels (defined in the .hip translation units)
 __global__ void preprocess_kernel(PreprocessArgs a);
 __global__ void mark_visible_kernel(int P, const float* means3D, const float* view, uint8_t* present);
-__global__ void duplicate_in_depth_order_kernel(int P, const uint32_t* order, const uint32_t* depth_scan,
-                                                const float2* means2D, const int* radii, int grid_x, int grid_y,
-                                                uint32_t* tile_keys, uint32_t* gid_out, const uint32_t* offsets,
-                                                float4* records, int rec4);
-__global__ void identify_ranges_kernel(int L, const uint32_t* tiles, uint2* ranges);
+__global__ void duplicate_kernel(int P, const uint32_t* offsets, const float2* means2D, const int* radii, int grid_x,
+                                 int grid_y, uint32_t* tile_keys, uint32_t* gid_out, uint32_t* flags, float4* records,
+                                 int rec4);
+__global__ void tile_ranges_kernel(int T, int L, const uint32_t* tiles, uint2* ranges);
+__global__ void tile_depth_sort_kernel(int T, const uint2* ranges, const uint32_t* order, const uint32_t* depth_keys,
+                                       uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB);
 
 // Slot of an instance from its Gaussian's render record word 1 (x, y, slot0, radius) and its tile.
 __device__ __forceinline__ uint32_t record_slot(float4 r1, int tx, int ty, int grid_x, int grid_y) {
@@ -197,7 +197,7 @@ hipError_t launch_gather_backward(const GatherBwdArgs& a, hipStream_t stream);
 // render record the blend kernels stage from: float4 [conic.x, conic.y, conic.z, opacity],
 // float4 [x, y, slot0 bits, radius bits], then the attribute row [r, g, b, depth, f0 .. f_{SMAX-1}]
 // zero-padded to (4 + SMAX + 3) / 4 float4. slot0 = offsets[g-1] (the Gaussian's first unsorted
-// slot). Written by preprocess_kernel (+ slot0 by duplicate_in_depth_order_kernel) for visible
+// slot). Written by preprocess_kernel (+ slot0 by duplicate_kernel) for visible
 // Gaussians only; the blend kernels never stage an invisible one.
 __host__ __device__ inline int smax_of(int S) {
     return S == 0 ? 0 : S <= 4 ? 4 : S <= 8 ? 8 : S <= 12 ? 12 : S <= 16 ? 16 : S <= 24 ? 24 : 32;

@@ -68,29 +68,9 @@ static size_t sort_temp_size(size_t L) {  // tile sort of the instances
     return bytes;
 }
 
-static size_t depth_sort_temp_size(size_t P) {  // depth sort of the Gaussians
-    size_t bytes = 0;
-    uint32_t* k = nullptr;
-    rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, k, k, rocprim::counting_iterator<uint32_t>(0), k, P, 0,
-                                          32, 0);
-    return bytes;
-}
-
 static bool use_tile_order() {
     const char* e = getenv("R3DG_TILE_ORDER");
     return !(e && e[0] == 'x');  // backward: "xcd" = spatial XCD-aware order; default longest first
-}
-
-static auto depth_order_touched(const uint32_t* touched, const uint32_t* order) {
-    return rocprim::make_transform_iterator(rocprim::counting_iterator<uint32_t>(0),
-                                            TouchedInDepthOrder{touched, order});
-}
-
-static size_t depth_scan_temp_size(size_t P) {
-    size_t bytes = 0;
-    uint32_t* d = nullptr;
-    rocprim::inclusive_scan(nullptr, bytes, depth_order_touched(d, d), d, P, rocprim::plus<uint32_t>(), 0);
-    return bytes;
 }
 
 // Carving works on an integer cursor so the same code computes sizes (base 0) and pointers.
@@ -116,15 +96,8 @@ static GeomState carve_geom(uintptr_t p, size_t P, int S, uintptr_t* end) {
     g.tiles_touched = carve<uint32_t>(p, P);
     g.point_offsets = carve<uint32_t>(p, P);
     g.depth_keys = carve<uint32_t>(p, P);
-    g.depth_keys_sorted = carve<uint32_t>(p, P);
-    g.depth_order = carve<uint32_t>(p, P);
-    g.depth_scan = carve<uint32_t>(p, P);
     g.scan_temp_bytes = scan_temp_size(P);
     g.scan_temp = carve<char>(p, g.scan_temp_bytes);
-    g.depth_sort_temp_bytes = depth_sort_temp_size(P);
-    g.depth_sort_temp = carve<char>(p, g.depth_sort_temp_bytes);
-    g.depth_scan_temp_bytes = depth_scan_temp_size(P);
-    g.depth_scan_temp = carve<char>(p, g.depth_scan_temp_bytes);
     // render records last: every other offset is independent of S
     g.records = S >= 0 ? carve<float4>(p, P * (size_t)record_f4(S)) : nullptr;
     if (end) *end = p;
@@ -143,6 +116,8 @@ static BinningState carve_binning(uintptr_t p, size_t L, uintptr_t* end) {
     b.tile_sorted = carve<uint32_t>(p, L);
     b.gid_in = carve<uint32_t>(p, L);
     b.point_list = carve<uint32_t>(p, L);
+    b.keys2 = carve<uint32_t>(p, L);
+    b.flags = carve<uint32_t>(p, L);
     b.sort_temp_bytes = sort_temp_size(L);
     b.sort_temp = carve<char>(p, b.sort_temp_bytes);
     if (end) *end = p;
@@ -588,27 +563,13 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         size_t tb = geom.scan_temp_bytes;
         R3DG_CHECK_HIP(rocprim::inclusive_scan(geom.scan_temp, tb, geom.tiles_touched, geom.point_offsets,
                                                (size_t)P, rocprim::plus<uint32_t>(), st));
-        // num_rendered (rasterizer_impl.cu:259-263 reads it with a blocking cudaMemcpy): copied into
-        // pinned host memory right after the scan; the host then waits on an event behind that copy
-        // only, so its wake-up overlaps the depth sort enqueued below instead of idling the GPU
+        // num_rendered (rasterizer_impl.cu:259-263 reads it with a blocking cudaMemcpy): one 4-byte
+        // copy into pinned host memory and a wait on an event behind that copy only
         Readback* rb = nullptr;
         R3DG_CHECK_HIP(readback_slot(&rb));
         R3DG_CHECK_HIP(hipMemcpyAsync(rb->host, geom.point_offsets + P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                       st));
         R3DG_CHECK_HIP(hipEventRecord(rb->ev, st));
-        {
-            // Gaussians by ascending depth bits, stable (ties keep ascending id), then the
-            // instance offsets in that order; both overlap the host read of num_rendered below
-            ProfScope ps(R3DG_PROF_SORT, st, true);
-            size_t db = geom.depth_sort_temp_bytes;
-            R3DG_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(geom.depth_sort_temp, db, geom.depth_keys,
-                                                     geom.depth_keys_sorted, rocprim::counting_iterator<uint32_t>(0),
-                                                     geom.depth_order, (size_t)P, 0, 32, st));
-            size_t sb2 = geom.depth_scan_temp_bytes;
-            R3DG_CHECK_HIP(rocprim::inclusive_scan(geom.depth_scan_temp, sb2,
-                                                   depth_order_touched(geom.tiles_touched, geom.depth_order),
-                                                   geom.depth_scan, (size_t)P, rocprim::plus<uint32_t>(), st));
-        }
         R3DG_CHECK_HIP(hipEventSynchronize(rb->ev));
         const uint32_t Lh = *rb->host;
         R3DG_REQUIRE(Lh < (1u << 31), "rasterize_gaussians: too many tile instances");
@@ -621,14 +582,15 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         return R3DG_ERR_ALLOC;
     }
     BinningState bin = binning_state_from(bin_base, (size_t)L);
-    R3DG_CHECK_HIP(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)T, st));
     if (L > 0) {
-        hipLaunchKernelGGL(duplicate_in_depth_order_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P,
-                           geom.depth_order, geom.depth_scan, geom.means2D, radii, gx, gy, bin.tile_keys,
-                           bin.gid_in, geom.point_offsets, geom.records, record_f4(S));
+        // duplicateWithKeys in the reference's Gaussian-major slot order (also zeroes the
+        // backward's row flags), stable sort by tile over bits [0, msb(T)), then every tile stably
+        // by depth: the reference's 45-bit stable sort of (tile << 32 | depth bits)
+        // (rasterizer_impl.cu:366-374) without a 64-bit key over L
+        hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, geom.point_offsets,
+                           geom.means2D, radii, gx, gy, bin.tile_keys, bin.gid_in, bin.flags, geom.records,
+                           record_f4(S));
         R3DG_CHECK_LAUNCH(s->debug, st);
-        // the reference sorts (tile << 32 | depth) over bits [0, 32 + msb(T)) (rasterizer_impl.cu:366-374);
-        // the depth part is already in order, so the tile bits [0, msb(T)) suffice
         const int bit = (int)higher_msb((uint32_t)T);
         size_t sb = bin.sort_temp_bytes;
         {
@@ -636,13 +598,21 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
             R3DG_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(bin.sort_temp, sb, bin.tile_keys, bin.tile_sorted,
                                                                  bin.gid_in, bin.point_list, (size_t)L, 0, bit, st));
         }
-        hipLaunchKernelGGL(identify_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, st, L, bin.tile_sorted,
+    }
+    // tile ranges for every tile (empty ones included: no memset), then the longest-first tile
+    // order the depth sort and the backward launch in
+    const bool order_tiles = use_tile_order();
+    if (T > 0) {
+        hipLaunchKernelGGL(tile_ranges_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, L, bin.tile_sorted,
                            img.ranges);
         R3DG_CHECK_LAUNCH(s->debug, st);
-    }
-    const bool order_tiles = use_tile_order();
-    {  // always computed (cheap), so a backward may use it whatever the forward's setting
         hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, T, img.ranges, img.tile_order);
+        R3DG_CHECK_LAUNCH(s->debug, st);
+    }
+    if (L > 0) {
+        ProfScope ps(R3DG_PROF_SORT, st, true);
+        hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(T), dim3(256), 0, st, T, img.ranges, img.tile_order,
+                           geom.depth_keys, bin.point_list, bin.tile_keys, bin.gid_in, bin.keys2);
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
@@ -778,22 +748,19 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     ImageState is = image_state_from(image, H, W);
     const int* radii = radii_in ? radii_in : gs.internal_radii;
     const int RS = part_row_stride(S);
-    // scratch: partial rows [4L, RS] (one per instance and quadrant, written sparsely), per-Gaussian
-    // sums [P, RS], one zero row (the gather's load target for absent rows), flags [4L]; the zero
-    // row and the flags are cleared by one memset
+    // scratch: partial rows [4L, RS] (one per instance and quadrant, written sparsely) and the
+    // per-Gaussian sums [P, RS]; the rows' presence flags live in the binning state, zeroed by the
+    // forward's duplicate pass (a row's presence depends on the forward state only)
     const size_t row_bytes = sizeof(float) * (size_t)RS * 4 * L;
     const size_t sum_bytes = sizeof(float) * (size_t)RS * P;
-    const size_t zero_bytes = sizeof(float) * (size_t)RS;
-    char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + sum_bytes + zero_bytes + 4 * (size_t)L);
+    char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + sum_bytes);
     if (!scratch) {
         set_error("rasterize_gaussians_backward: scratch allocation failed");
         return R3DG_ERR_ALLOC;
     }
     float* rows = L > 0 ? reinterpret_cast<float*>(scratch) : nullptr;
     float* sums = reinterpret_cast<float*>(scratch + row_bytes);
-    float* zero_row = reinterpret_cast<float*>(scratch + row_bytes + sum_bytes);
-    uint8_t* flags = reinterpret_cast<uint8_t*>(scratch + row_bytes + sum_bytes + zero_bytes);
-    R3DG_CHECK_HIP(hipMemsetAsync(zero_row, 0, zero_bytes + 4 * (size_t)L, st));
+    uint8_t* flags = reinterpret_cast<uint8_t*>(bs.flags);
     if (L > 0) {
         RenderBwdArgs ba{};
         ba.records = gs.records;
@@ -836,7 +803,6 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     ga.P = P; ga.D = s->D; ga.M = s->M; ga.S = S; ga.RS = RS;
     ga.W = W; ga.H = H; ga.grid_x = gx; ga.grid_y = gy;
     ga.rows = rows;
-    ga.zero_row = zero_row;
     ga.sums = sums;
     ga.flags = reinterpret_cast<const uint32_t*>(flags);
     ga.means2D = gs.means2D;

@@ -819,8 +819,8 @@ __device__ __forceinline__ void gather_gaussian(const GatherBwdArgs& a, int g, c
 // same fixed order every run). One group of LPG lanes per Gaussian. The Gaussian's rows are the
 // contiguous range 4 * [k0, k1) (row 4 * slot + quadrant); per chunk of 8 slots, lanes 0..7 load
 // one flag word each and the group ORs them into a 32-bit (slot, quadrant) presence mask, then
-// walks the present rows four at a time with independent loads (absent tail rows read the shared
-// zero row). Lane c loads float4 column c of every row: c < NXC sums the X part; c == NXC expands
+// walks the present rows four at a time with independent loads (absent tail rows load nothing).
+// Lane c loads float4 column c of every row: c < NXC sums the X part; c == NXC expands
 // each row's quadrant-centred moments [S0, Sx, Sy, Sxx] about the Gaussian's mean (dx = mean.x -
 // pixel.x = d0x - x with d0x = mean.x - quadrant centre); c == NXC + 1 sums [Sxy, Syy], the
 // moments whose expansion needs no coefficient. Writes sums + g * RS = [X part (XW) | dL/dmean2D
@@ -863,9 +863,10 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 bit[i] = mask ? __builtin_ctz(mask) : 0;
-                const float* row = mask ? base + (size_t)bit[i] * RS : a.zero_row;
+                const bool has = mask != 0u;
+                const float* row = base + (size_t)bit[i] * RS;
                 mask &= mask - 1u;
-                v[i] = active ? reinterpret_cast<const float4*>(row)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[i] = active && has ? reinterpret_cast<const float4*>(row)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
             if (c < NXC || c == NXC + 1) {
 #pragma unroll
@@ -878,7 +879,7 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
                     // tile of slot kb + bit/4 in the row-major rect (slot order = duplicateWithKeys)
                     const int idx = (int)kb + (bit[i] >> 2), q = bit[i] & 3;
                     const int iy = (int)(((float)idx + 0.5f) * inv_rw), ix = idx - iy * rw;
-                    const float4 m = v[i];  // S0 Sx Sy Sxx (zero for the zero row)
+                    const float4 m = v[i];  // S0 Sx Sy Sxx (zero for an absent row)
                     const float d0x = xy.x - ((float)((x0 + ix) * kTileX + (q & 1) * 8) + 3.5f);
                     const float d0y = xy.y - ((float)((y0 + iy) * kTileY + (q >> 1) * 8) + 3.5f);
                     S0 += m.x;

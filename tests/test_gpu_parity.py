@@ -87,6 +87,27 @@ def test_forward_pseudo_normal_and_xyz(hip_ext):
     assert_close("normal", hn[solid], on[solid], 1e-4, 1e-4)
 
 
+def test_dense_tiles_depth_sort(hip_ext):
+    """Tiles far longer than one depth-sort chunk (preprocess.hip tile_depth_sort_kernel: 1024
+    instances; longer tiles merge sorted runs) with many exact depth ties (the reference orders
+    ties by Gaussian id): keys, point list and ranges bit-exact, images within 1e-4."""
+    scene, cam = synthetic.small_scene(P=40000, S=11, seed=40, width=64, height=48, scale_range=(0.02, 0.12))
+    m = scene.means3D.copy()
+    m[:, 2] = np.round(m[:, 2] * 4.0) / 4.0  # 15 distinct depths: thousands of ties per tile
+    m[:, :2] *= (m[:, 2] / scene.means3D[:, 2])[:, None]
+    scene = synthetic.Scene(m, scene.scales, scene.rotations, scene.opacity, scene.sh, scene.features)
+    h = hip_forward(hip_ext, scene, cam, S=11)
+    o = _oracle_fwd(scene, cam, 11)
+    counts = o["ranges"][:, 1].astype(np.int64) - o["ranges"][:, 0]
+    assert counts.max() > 4 * 1024, counts.max()  # at least three merge rounds
+    _check_forward(h, o, 11)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=6)
+    gh = hip_backward(hip_ext, h, dc, do, dd, df)
+    go = oracle.rasterize_backward(o, dc, do, dd, df)
+    for k in ["dL_dmeans2D", "dL_dopacity", "dL_dfeatures", "dL_dmeans3D", "dL_dsh"]:
+        assert_close(k, gh[k], go[k], _grad_tol(go[k]), 2e-3)
+
+
 def test_cull_is_exact(hip_ext):
     """The per-quadrant footprint skip must not change a single bit (render_fwd.hip)."""
     scene, cam = synthetic.small_scene(P=5000, S=11, seed=3, width=128, height=96, scale_range=(0.005, 0.3))
