@@ -4,9 +4,10 @@ Workload (BASELINE.json metric, SURVEY.md §8d "M1"): 1,000,000 synthetic Gaussi
 S=11 features, SH degree 3, default shaders, pseudo normal on, backward_geometry on; upstream
 gradients N(0,1)*1e-3 in the reference's CHW contract. One step = one view: the reference's
 `_C.rasterize_gaussians` then `_C.rasterize_gaussians_backward` through this build's `_C`, and,
-when N > 1, one RCCL all-reduce of the flat per-Gaussian gradient buffer (70 floats/Gaussian:
-means3D 3 + sh 48 + opacity 1 + scales 3 + rotations 4 + features 11) -- view-parallel data
-parallelism, every rank renders its own camera of the same scene (weak scaling).
+when N > 1, the per-Gaussian gradient exchange (view_parallel.py: RCCL all-reduce of means3D 3 + opacity 1 +
+scales 3 + rotations 4 + features 11 floats, all-gather of each view's 3-float SH colour gradient,
+the 48-float SH gradient sum rebuilt on every rank) -- view-parallel data parallelism, every rank
+renders its own camera of the same scene (weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
@@ -357,7 +358,8 @@ def main() -> None:
         "config": {"workload": "M1: rasterize_gaussians + rasterize_gaussians_backward, 1M Gaussians, 1920x1080, "
                                "S=11 features, SH degree 3, default shaders, pseudo normal",
                    "gaussians": args.P, "width": W, "height": H, "features": S_M1, "num_rendered": int(L),
-                   "parallelism": f"view-parallel dp{world} (RCCL all-reduce of 70 floats/Gaussian, "
+                   "parallelism": f"view-parallel dp{world} (per Gaussian: RCCL all-reduce of 22 floats + "
+                                  f"all-gather of the 3-float SH colour gradient, SH sum rebuilt per rank; "
                                   f"{args.chunks} chunks overlapped with the gather phase)"},
         "views_per_s": round(world * args.steps / elapsed, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

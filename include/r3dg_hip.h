@@ -170,6 +170,20 @@ int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* settings, cons
                                       r3dg_alloc_fn scratch_alloc, void* scratch_ctx,
                                       const r3dg_backward_outputs* out, r3dg_stream_t stream);
 
+/* View-parallel SH-gradient exchange (relightable3dgaussian_amd/view_parallel.py). The SH part of
+ * a view's gradient is rank-1 per Gaussian: dL/dsh[k][c] = Y_k(dir) * dRGB[c] with dir =
+ * normalize(mean - campos) and dRGB the clamp-masked colour gradient (backward.cu:20-139). So
+ * instead of all-reducing 3*M floats per Gaussian, ranks all-gather dRGB (3 floats) and every
+ * rank rebuilds the sum over views.
+ *   r3dg_sh_color_grads: dRGB of Gaussians [g0, g0 + n) of this view: dL_dcolors (the backward's
+ *     output) with the channels whose SH colour the forward clamped at 0 zeroed (geom state).
+ *   r3dg_sh_grad_from_views: dL_dsh rows [g0, g0 + n) = sum over the N views, in view order, of
+ *     Y_k(normalize(mean - campos[v])) * drgb[v][i][c] for k < (degree+1)^2, 0 for k < M beyond;
+ *     drgb is [N][n][3] (the views' dRGB of these Gaussians), campos [N][3]. */
+int r3dg_sh_color_grads(int P, int g0, int n, void* geom, const float* dL_dcolors, float* drgb, r3dg_stream_t stream);
+int r3dg_sh_grad_from_views(int g0, int n, int degree, int M, int N, const float* means3D, const float* campos,
+                            const float* drgb, float* dL_dsh, r3dg_stream_t stream);
+
 /* markVisible (rasterize_points.cu:277-295): present[i] = view-space z > 0.2 */
 int r3dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                       uint8_t* present, r3dg_stream_t stream);

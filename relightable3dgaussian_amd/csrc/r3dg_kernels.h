@@ -189,6 +189,9 @@ hipError_t launch_render_forward(const RenderFwdArgs& a, bool shader, hipStream_
 hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t stream);
 hipError_t launch_row_sum(const GatherBwdArgs& a, hipStream_t stream);
 hipError_t launch_gather_backward(const GatherBwdArgs& a, hipStream_t stream);
+hipError_t launch_sh_color_grads(int n, const uint8_t* clamped, const float* dcol, float* out, hipStream_t st);
+hipError_t launch_sh_grad_views(int g0, int n, int deg, int M, int N, const float* means3D, const float* campos,
+                                const float* drgb, float* dsh, hipStream_t st);
 
 // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so block b runs on the
 // same XCD as b+8. Give each XCD a contiguous band of tiles (neighbouring tiles share

@@ -854,6 +854,24 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     return R3DG_OK;
 }
 
+extern "C" int r3dg_sh_color_grads(int P, int g0, int n, void* geom, const float* dL_dcolors, float* drgb,
+                                   r3dg_stream_t stream) {
+    R3DG_REQUIRE(P >= 0 && g0 >= 0 && n >= 0 && g0 + n <= P && geom && (n == 0 || (dL_dcolors && drgb)),
+                 "sh_color_grads: invalid arguments");
+    const GeomState gs = geom_state_from(geom, (size_t)P);
+    R3DG_CHECK_HIP(launch_sh_color_grads(n, gs.clamped + g0, dL_dcolors + 3 * (size_t)g0, drgb, (hipStream_t)stream));
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_sh_grad_from_views(int g0, int n, int degree, int M, int N, const float* means3D,
+                                       const float* campos, const float* drgb, float* dL_dsh, r3dg_stream_t stream) {
+    R3DG_REQUIRE(g0 >= 0 && n >= 0 && N >= 1 && degree >= 0 && degree <= 3 && (degree + 1) * (degree + 1) <= M &&
+                     M <= 16 && (n == 0 || (means3D && campos && drgb && dL_dsh)),
+                 "sh_grad_from_views: invalid arguments (degree 0..3, (degree+1)^2 <= M <= 16)");
+    R3DG_CHECK_HIP(launch_sh_grad_views(g0, n, degree, M, N, means3D, campos, drgb, dL_dsh, (hipStream_t)stream));
+    return R3DG_OK;
+}
+
 extern "C" int r3dg_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                                  uint8_t* present, r3dg_stream_t stream) {
     (void)projmatrix;

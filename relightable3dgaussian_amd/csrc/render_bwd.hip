@@ -592,15 +592,15 @@ hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t stream) {
 // per-Gaussian: sum of gradient rows + preprocessing backward
 // ---------------------------------------------------------------------------------------------
 
-// backward.cu:20-139 (computeColorFromSH backward). dL_dRGB already clamp-masked.
-__device__ static void sh_backward(int deg, int M, float3 pos, const float* campos, const float* sh,
-                                   const float* dRGB, float* dL_dmean, float* dsh) {
-    const float dox = pos.x - campos[0], doy = pos.y - campos[1], doz = pos.z - campos[2];
+// The view direction of a Gaussian and its SH basis (backward.cu:27-57): shared by sh_backward
+// and the view-parallel SH rebuild, so both evaluate the same expressions to the same bits.
+__device__ __forceinline__ void sh_dir_basis(float3 pos, const float* campos, float& dox, float& doy, float& doz,
+                                             float& x, float& y, float& z, float* b) {
+#pragma clang fp contract(off)
+    dox = pos.x - campos[0]; doy = pos.y - campos[1]; doz = pos.z - campos[2];
     const float len = sqrtf(dox * dox + doy * doy + doz * doz);
-    const float x = dox / len, y = doy / len, z = doz / len;
+    x = dox / len; y = doy / len; z = doz / len;
     const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-    float ddx[3] = {0.f, 0.f, 0.f}, ddy[3] = {0.f, 0.f, 0.f}, ddz[3] = {0.f, 0.f, 0.f};
-    float b[16];
     b[0] = SH_C0;
     b[1] = -SH_C1 * y; b[2] = SH_C1 * z; b[3] = -SH_C1 * x;
     b[4] = SH_C2_0 * xy; b[5] = SH_C2_1 * yz; b[6] = SH_C2_2 * (2.f * zz - xx - yy); b[7] = SH_C2_3 * xz;
@@ -608,6 +608,15 @@ __device__ static void sh_backward(int deg, int M, float3 pos, const float* camp
     b[9] = SH_C3_0 * y * (3.f * xx - yy); b[10] = SH_C3_1 * xy * z; b[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
     b[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy); b[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
     b[14] = SH_C3_5 * z * (xx - yy); b[15] = SH_C3_6 * x * (xx - 3.f * yy);
+}
+
+// backward.cu:20-139 (computeColorFromSH backward). dL_dRGB already clamp-masked.
+__device__ static void sh_backward(int deg, int M, float3 pos, const float* campos, const float* sh,
+                                   const float* dRGB, float* dL_dmean, float* dsh) {
+    float dox, doy, doz, x, y, z, b[16];
+    sh_dir_basis(pos, campos, dox, doy, doz, x, y, z, b);
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    float ddx[3] = {0.f, 0.f, 0.f}, ddy[3] = {0.f, 0.f, 0.f}, ddz[3] = {0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         if (deg > 0) {
@@ -641,7 +650,7 @@ __device__ static void sh_backward(int deg, int M, float3 pos, const float* camp
     const int ncoef = deg > 2 ? 16 : (deg > 1 ? 9 : (deg > 0 ? 4 : 1));
     for (int i = 0; i < M; ++i)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) dsh[3 * i + c] = i < ncoef ? b[i] * dRGB[c] : 0.f;
+        for (int c = 0; c < 3; ++c) dsh[3 * i + c] = i < ncoef ? __fmul_rn(b[i], dRGB[c]) : 0.f;
     const float dvx = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
     const float dvy = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
     const float dvz = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
@@ -813,6 +822,69 @@ __device__ __forceinline__ void gather_gaussian(const GatherBwdArgs& a, int g, c
         for (int i = 0; i < 3; ++i) a.dL_dscales[3 * g + i] = 0.f;
         for (int i = 0; i < 4; ++i) a.dL_drotations[4 * g + i] = 0.f;
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// View-parallel SH-gradient exchange (include/r3dg_hip.h r3dg_sh_color_grads / _from_views)
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sh_color_grads_kernel(int n, const uint8_t* __restrict__ clamped,
+                                                             const float* __restrict__ dcol, float* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= 3 * n) return;
+    const int g = i / 3, c = i - 3 * g;
+    out[i] = ((clamped[g] >> c) & 1) ? 0.f : dcol[i];
+}
+
+// One thread per Gaussian: the SH basis of each view's direction exactly as sh_backward computes
+// it (backward.cu:20-139), summed over the views in order.
+__global__ void __launch_bounds__(256) sh_grad_views_kernel(int g0, int n, int deg, int M, int N,
+                                                            const float* __restrict__ means3D,
+                                                            const float* __restrict__ campos,
+                                                            const float* __restrict__ drgb, float* __restrict__ dsh) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int g = g0 + i;
+    const float px = means3D[3 * g], py = means3D[3 * g + 1], pz = means3D[3 * g + 2];
+    const int ncoef = deg > 2 ? 16 : (deg > 1 ? 9 : (deg > 0 ? 4 : 1));
+    float acc[16][3];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[k][0] = acc[k][1] = acc[k][2] = 0.f;
+    const float3 pos = make_float3(px, py, pz);
+    for (int v = 0; v < N; ++v) {
+        float dox, doy, doz, x, y, z, b[16];
+        sh_dir_basis(pos, campos + 3 * v, dox, doy, doz, x, y, z, b);
+        const float* d = drgb + ((size_t)v * n + i) * 3;
+        const float d0 = d[0], d1 = d[1], d2 = d[2];
+        // each view's product rounded as sh_backward rounds it, then summed in view order
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            acc[k][0] = __fadd_rn(acc[k][0], __fmul_rn(b[k], d0));
+            acc[k][1] = __fadd_rn(acc[k][1], __fmul_rn(b[k], d1));
+            acc[k][2] = __fadd_rn(acc[k][2], __fmul_rn(b[k], d2));
+        }
+    }
+    float* o = dsh + (size_t)g * M * 3;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < M) {
+            const bool on = k < ncoef;
+            o[3 * k] = on ? acc[k][0] : 0.f;
+            o[3 * k + 1] = on ? acc[k][1] : 0.f;
+            o[3 * k + 2] = on ? acc[k][2] : 0.f;
+        }
+}
+
+hipError_t launch_sh_color_grads(int n, const uint8_t* clamped, const float* dcol, float* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sh_color_grads_kernel, dim3((3 * n + 255) / 256), dim3(256), 0, st, n, clamped, dcol, out);
+    return hipGetLastError();
+}
+hipError_t launch_sh_grad_views(int g0, int n, int deg, int M, int N, const float* means3D, const float* campos,
+                                const float* drgb, float* dsh, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sh_grad_views_kernel, dim3((n + 255) / 256), dim3(256), 0, st, g0, n, deg, M, N, means3D,
+                       campos, drgb, dsh);
+    return hipGetLastError();
 }
 
 // Gather phase 1: per-Gaussian sums of its partial rows, in slot order then quadrant order (the

@@ -287,6 +287,38 @@ BwdResult rasterize_gaussians_backward_chunked(
                          backward_geometry, debug, (int)H, (int)W, color_hwc, feature_native, (int)n_chunks, chunk_cb);
 }
 
+// View-parallel SH-gradient exchange (include/r3dg_hip.h): this view's clamp-masked colour
+// gradients of Gaussians [g0, g1) (the rank's all-gather payload) ...
+torch::Tensor sh_color_grads(const torch::Tensor& geomBuffer, int64_t P, const torch::Tensor& dL_dcolors, int64_t g0,
+                             int64_t g1) {
+    const torch::Device dev = dL_dcolors.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    TORCH_CHECK(dev.is_cuda() && dL_dcolors.is_contiguous() && dL_dcolors.numel() == 3 * P && 0 <= g0 && g0 <= g1 &&
+                    g1 <= P, "sh_color_grads: dL_dcolors must be a contiguous CUDA [P,3] tensor, 0 <= g0 <= g1 <= P");
+    auto out = torch::empty({g1 - g0, 3}, dL_dcolors.options());
+    check(r3dg_sh_color_grads((int)P, (int)g0, (int)(g1 - g0), geomBuffer.data_ptr(), dL_dcolors.data_ptr<float>(),
+                              out.data_ptr<float>(), stream_of(dev)),
+          "sh_color_grads");
+    return out;
+}
+
+// ... and the sum over the N views of their SH gradients, rebuilt from the gathered [N, n, 3]
+// colour gradients and the views' camera centres [N, 3], into rows [g0, g0 + n) of dL_dsh.
+void sh_grad_from_views(const torch::Tensor& means3D, const torch::Tensor& campos, const torch::Tensor& drgb,
+                        int64_t degree, int64_t g0, torch::Tensor& dL_dsh) {
+    const torch::Device dev = means3D.device();
+    const c10::OptionalDeviceGuard guard(dev);
+    TORCH_CHECK(drgb.dim() == 3 && drgb.size(2) == 3 && campos.dim() == 2 && campos.size(1) == 3 &&
+                    campos.size(0) == drgb.size(0) && dL_dsh.dim() == 3 && dL_dsh.size(2) == 3 &&
+                    dL_dsh.is_contiguous() && g0 >= 0 && g0 + drgb.size(1) <= dL_dsh.size(0),
+                "sh_grad_from_views: drgb [N,n,3], campos [N,3], dL_dsh [P,M,3] contiguous");
+    auto m3 = dev_contig(means3D, dev), cp = dev_contig(campos, dev), d = dev_contig(drgb, dev);
+    check(r3dg_sh_grad_from_views((int)g0, (int)drgb.size(1), (int)degree, (int)dL_dsh.size(1), (int)drgb.size(0),
+                                  m3.data_ptr<float>(), cp.data_ptr<float>(), d.data_ptr<float>(),
+                                  dL_dsh.data_ptr<float>(), stream_of(dev)),
+          "sh_grad_from_views");
+}
+
 torch::Tensor mark_visible(torch::Tensor& means3D, torch::Tensor& viewmatrix, torch::Tensor& projmatrix) {
     const torch::Device dev = means3D.device();
     const c10::OptionalDeviceGuard guard(dev);
@@ -810,6 +842,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("rasterize_gaussians_backward_chunked", &rasterize_gaussians_backward_chunked);
     m.def("render_equation_forward_with_rand", &render_equation_forward_with_rand);
     m.def("rasterizer_state", &rasterizer_state);
+    m.def("sh_color_grads", &sh_color_grads);
+    m.def("sh_grad_from_views", &sh_grad_from_views);
     m.def("feature_groups", &feature_groups);
     m.def("create_shader_manager", &create_shader_manager);
     m.def("shader_manager_info", &shader_manager_info);

@@ -492,7 +492,7 @@ def test_backward_chunked_delivery(hip_ext):
         np.testing.assert_array_equal(out[i].cpu().numpy().reshape(ref[k].shape), ref[k], err_msg=k)
 
 
-def _chunked_exchange_worker(rank, world, port, q):
+def _chunked_exchange_worker(rank, world, port, q, mode="views"):
     import torch
     import torch.distributed as dist
 
@@ -511,7 +511,7 @@ def _chunked_exchange_worker(rank, world, port, q):
             a["cov3D"], tt(cam.view), tt(cam.proj), cam.tanfovx, cam.tanfovy, tt(dc), tt(do), tt(dd), tt(df), a["sh"],
             3, tt(cam.campos), h["geom"], h["num_rendered"], h["binning"], h["image"], True, False, cam.height,
             cam.width, False, False)
-    out = view_parallel.backward_all_reduce(r3._C, args, n_chunks=4)
+    out = view_parallel.backward_all_reduce(r3._C, args, n_chunks=4, sh_exchange=mode)
     torch.cuda.synchronize()
     res = {name: out[i].cpu().numpy() for name, i in view_parallel.GRAD_FIELDS}
     q.put((rank, res, {"means3D": local["dL_dmeans3D"], "sh": local["dL_dsh"], "opacity": local["dL_dopacity"],
@@ -520,9 +520,12 @@ def _chunked_exchange_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_view_parallel_chunked_exchange_two_ranks(hip_ext):
+@pytest.mark.parametrize("mode", ["views", "allreduce"])
+def test_view_parallel_chunked_exchange_two_ranks(hip_ext, mode):
     """bench.py's N > 1 path on one GPU: two gloo ranks render the same view, the chunked
-    all-reduce (overlapped with the gather phase) must return exactly 2x the local gradients."""
+    exchange (overlapped with the gather phase) must return exactly 2x the local gradients --
+    also the SH block rebuilt from the all-gathered colour gradients ("views": each view's
+    product rounded as the backward rounds it, summed in view order)."""
     import multiprocessing as mp
     import socket
 
@@ -531,7 +534,7 @@ def test_view_parallel_chunked_exchange_two_ranks(hip_ext):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    procs = [ctx.Process(target=_chunked_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_chunked_exchange_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     got = [q.get(timeout=180) for _ in procs]
@@ -540,3 +543,39 @@ def test_view_parallel_chunked_exchange_two_ranks(hip_ext):
     for rank, res, local in got:
         for k, v in res.items():
             np.testing.assert_array_equal(v.reshape(local[k].shape), 2 * local[k], err_msg=f"rank {rank} {k}")
+
+
+def test_sh_rebuild_kernels_match_oracle(hip_ext):
+    """r3dg_sh_color_grads + r3dg_sh_grad_from_views (the view-parallel SH exchange) against
+    oracle/view_exchange.py and the sum of the C oracle's per-view dL_dsh, three views, chunked
+    rows."""
+    import torch
+
+    from oracle import view_exchange
+    from relightable3dgaussian_amd import view_parallel
+
+    base = synthetic.m1_camera(96, 64)
+    scene = synthetic.m1_scene(P=3000, S=11, seed=12, cam=base)
+    drgb, cams, per_view_sh = [], [], []
+    for r in range(3):
+        cam = view_parallel.rank_camera(base, r, 3, step_deg=5.0)
+        h = hip_forward(hip_ext, scene, cam, S=11)
+        dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=20 + r)
+        g = hip_backward(hip_ext, h, dc, do, dd, df)
+        o = _oracle_fwd(scene, cam, 11)
+        d = hip_ext.sh_color_grads(h["geom"], scene.P, tt(g["dL_dcolors"]), 0, scene.P)
+        np.testing.assert_array_equal(d.cpu().numpy(), view_exchange.sh_color_grads(g["dL_dcolors"], o["clamped"]))
+        drgb.append(d)
+        cams.append(np.asarray(cam.campos, np.float32))
+        per_view_sh.append(g["dL_dsh"])
+    P = scene.P
+    out = torch.full((P, 16, 3), float("nan"), device="cuda")
+    d_all = torch.stack(drgb)
+    for g0, g1 in [(0, 1024), (1024, 2048), (2048, P)]:
+        hip_ext.sh_grad_from_views(tt(scene.means3D), tt(np.stack(cams)), d_all[:, g0:g1].contiguous(), 3, g0, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    ref = view_exchange.sh_grad_from_views(scene.means3D, np.stack(cams), d_all.cpu().numpy(), 3, 16)
+    scale = float(np.abs(ref).max())
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6 * scale)
+    np.testing.assert_allclose(got, sum(per_view_sh), rtol=1e-5, atol=1e-6 * scale)
