@@ -364,7 +364,7 @@ def main() -> None:
         "views_per_s": round(world * args.steps / elapsed, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "renderCUDA fwd + bwd: render_fwd_kernel + render_bwd_mfma_kernel + row_sum_kernel",
+                     "kernel": "renderCUDA fwd + bwd: render_fwd_kernel + render_bwd_glds_kernel + row_sum_kernel",
                      "algorithmic_bytes": bf + bb, "kernel_ms": round(t_kern * 1e3, 4), "valu": valu},
         "kernel_ms": {k: round(v, 4) for k, v in avg.items() if prof[k][0]},
     }

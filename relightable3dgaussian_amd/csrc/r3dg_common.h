@@ -280,6 +280,19 @@ __device__ __forceinline__ float qform_min_rect(float a, float b, float c, float
     return fminf(fminf(edge_x(xa), edge_x(xb)), fminf(edge_y(ya), edge_y(yb)));
 }
 
+// quadrant_mask's test for one quadrant with top-left pixel (qx, qy): may alpha reach 1/255 there
+// (bit q of quadrant_mask(xy, co, x0, y0, cull) for qx = x0 + (q & 1) * 8, qy = y0 + (q >> 1) * 8).
+__device__ __forceinline__ bool quadrant_live(float2 xy, float4 co, float qx, float qy, int cull) {
+    if (!cull) return true;
+    if (co.w < 1.0f / 255.0f) return false;
+    const float det = co.x * co.z - co.y * co.y;
+    if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return true;
+    const float t = 2.0f * __logf(255.0f * co.w) * 1.1f + 0.1f;
+    if (!(t < 1e30f)) return true;
+    const float ia = __builtin_amdgcn_rcpf(co.x), ic = __builtin_amdgcn_rcpf(co.z);
+    return !(qform_min_rect(co.x, co.y, co.z, ia, ic, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f) > t);
+}
+
 // Conservative set of the 8x8 quadrants of tile (x0, y0) in which alpha = o exp(-Q/2) can reach
 // 1/255, i.e. Q <= 2 ln(255 o). A quadrant is dropped only if the minimum of Q over its pixel
 // rectangle exceeds t = 2 ln(255 o) * 1.1 + 0.1 -- the 10 % + 0.1 margin covers the fp32

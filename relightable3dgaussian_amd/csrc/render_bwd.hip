@@ -249,6 +249,9 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
+#ifndef R3DG_BWD_EARLY_ATTR
+#define R3DG_BWD_EARLY_ATTR 0  // glds kernel: a pair's attribute rows read before its exp (measured: no gain)
+#endif
 #ifndef R3DG_BWDW_NB
 #define R3DG_BWDW_NB 32  // instances staged per batch by a one-wave workgroup
 #endif
@@ -562,18 +565,298 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
 #endif
 }
 
+// ---------------------------------------------------------------------------------------------
+// Double-buffered variant: the render records of batch b+1 are copied HBM -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, no VGPRs) while the waves blend batch b, so the record round trip is
+// off the critical path and a batch costs one block barrier instead of two. Every wave evaluates
+// the quadrant cull of the staged instances for its own quadrant (ballot -> live mask in SGPRs)
+// and reads an instance's slot from the lane that computed it, so nothing but the records goes
+// through LDS. Staging buffer layout: column q (float4 q of the record) of instance t at
+// [q * NB + t], two columns per DMA wave-instruction (lanes 0-31 column 2k, lanes 32-63 column
+// 2k+1). Same blend step, MFMA flush and partial rows as render_bwd_mfma_kernel.
+// ---------------------------------------------------------------------------------------------
+template <int SMAX>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
+render_bwd_glds_kernel(RenderBwdArgs a) {
+    constexpr int NB = 32;                        // instances per batch (two batches staged)
+    constexpr int NA4 = (4 + SMAX + 3) / 4;
+    constexpr int NXB = (4 + SMAX + 15) / 16;
+    constexpr int XW = 16 * NXB;
+    constexpr int GRP = 16;
+    constexpr int RF4 = 2 + NA4;                  // float4s per render record
+    constexpr int NCP = (RF4 + 1) / 2;            // DMA wave-instructions per batch
+    constexpr int SBUF = 2 * NCP * NB;            // float4s per staging buffer
+    constexpr int WQF4 = 2 * GRP * WQS / 4;       // float4s per wave's w|q image
+    static_assert((2 * GRP * WQS) % 4 == 0, "w|q image must be float4-sized");
+    // one LDS array (a second __shared__ object can make the compiler wait for the DMA before
+    // unrelated LDS reads): [2 staging buffers | 4 w|q images | max_last]
+    __shared__ float4 s_lds[2 * SBUF + 4 * WQF4 + 1];
+
+    const int tile = block_tile(a.tile_order, a.num_tiles);
+    if (tile >= a.num_tiles) return;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    R3DG_BWD_PIXELS()
+    float T = T_final;
+    float* wq = reinterpret_cast<float*>(s_lds + 2 * SBUF + w * WQF4);
+    int* s_max_last = reinterpret_cast<int*>(s_lds + 2 * SBUF + 4 * WQF4);
+
+    float bX[NXB][16];
+    {
+#pragma unroll
+        for (int xb = 0; xb < NXB; ++xb) {
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                const int ch = xb * 16 + c;
+                float v = 0.f;
+                if (ch < 3) v = g[ch];
+                else if (ch - 3 < SMAX && ch - 3 < S) v = gf[(ch - 3) < SMAX ? (ch - 3) : 0];
+                else if (ch == 3 + S) v = gd;
+                wq[c * WQS + l] = v;
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
+            wave_lds_sync();
+        }
+    }
+    if (!a.backward_geometry) {
+#pragma unroll
+        for (int c = 0; c < SMAX; ++c) gf[c] = 0.f;
+    }
+    f32x2 gp[2 * NA4];
+#pragma unroll
+    for (int c2 = 0; c2 < 2 * NA4; ++c2) {
+        float e[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int ch = 2 * c2 + h;
+            e[h] = ch < 3 ? g[ch] : (ch == 3 ? gd : (ch - 4 < SMAX ? gf[(ch - 4) < SMAX ? ch - 4 : 0] : 0.f));
+        }
+        gp[c2] = f32x2{e[0], e[1]};
+    }
+    float u = 0.f;
+    const float TFB = T_final * bg_dot;
+    int rowj = 0;
+    const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
+    const int max_last = block_max_last(wmax, s_max_last);
+    const int RS = a.RS;
+    const int nch = l & 15;
+    const float4* st = s_lds;  // staging buffer of the current batch
+    const float qx0 = (float)(tx * kTileX + (w & 1) * 8), qy0 = (float)(ty * kTileY + (w >> 1) * 8);
+
+    auto attrs = [&](int j, float4* v4) {
+        const int ju = __builtin_amdgcn_readfirstlane(j);
+#pragma unroll
+        for (int q = 0; q < NA4; ++q) v4[q] = st[(2 + q) * NB + ju];
+    };
+    auto step = [&](const float4* v4, int p, bool live, float opacity, float power, float G, float& wv, float& qv) {
+#pragma clang fp contract(off)
+        float v[NA4 * 4];
+#pragma unroll
+        for (int q = 0; q < NA4; ++q) {
+            const float4 rr = v4[q];
+            v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
+        }
+        const float alpha = fminf(0.99f, opacity * G);
+        const bool ok = live && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const float ae = ok ? alpha : 0.f;
+        const float Ge = ok ? G : 0.f;
+        const float rinv = __builtin_amdgcn_rcpf(1.f - ae);
+        const float Tn = T * rinv;
+        f32x2 d2 = {go, 0.f};
+#pragma unroll
+        for (int c2 = 0; c2 < 2 * NA4; ++c2)
+            d2 = __builtin_elementwise_fma(f32x2{v[2 * c2], v[2 * c2 + 1]}, gp[c2], d2);
+        const float d = d2.x + d2.y;
+        const float diff = d - u;
+        const float dL_dalpha = rinv * __builtin_fmaf(T, diff, -TFB);
+        wv = ae * Tn;
+        qv = Ge * dL_dalpha;
+        T = Tn;
+        u = __builtin_fmaf(ae, diff, u);
+    };
+
+    auto flush = [&](int r) {
+        if (l == 0) R3DG_EXP_ADD(1, 1);
+        float yA[2], yB[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float xo = (float)(4 * h + (l >> 4)) - 3.5f;
+            yA[h] = nch == 0 ? 1.f : (nch == 1 ? xo : (nch == 3 ? xo * xo : 0.f));
+            yB[h] = nch == 2 ? 1.f : (nch == 4 ? xo : 0.f);
+        }
+        const float yC = nch == 5 ? 1.f : 0.f;
+        wave_lds_sync();
+        floatx4 accX[NXB], accY = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int xb = 0; xb < NXB; ++xb) accX[xb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+            const int col = 4 * s2 + (l >> 4);
+            const float av = wq[(l & 15) * WQS + col];
+            const float aq = wq[(GRP + (l & 15)) * WQS + col];
+#pragma unroll
+            for (int xb = 0; xb < NXB; ++xb)
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
+            const float yo = (float)(s2 >> 1) - 3.5f;
+            const float by = yA[s2 & 1] + yo * (yB[s2 & 1] + yo * yC);
+            accY = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, by, accY, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = (l >> 4) * 4 + i;
+            const uint32_t base = (uint32_t)__shfl(rowj, row);
+            if (row < r) {
+                float* dst = a.rows + (size_t)base * RS;
+#pragma unroll
+                for (int xb = 0; xb < NXB; ++xb) dst[xb * 16 + nch] = accX[xb][i];
+                if (nch < 6) dst[XW + nch] = accY[i];
+                if (nch == 0) a.flags[base] = 1;
+            }
+        }
+        wave_lds_sync();
+    };
+
+    // Gaussian of instance (l & 31) of the batch ending at tile position hi_b (tail lanes clamp
+    // to the batch's last instance, so every DMA lane reads a valid record)
+    auto batch_gid = [&](int hi_b) -> uint32_t {
+        const int tt = min(l & 31, min(NB, hi_b) - 1);
+        return a.point_list[range.x + (uint32_t)(hi_b - 1 - tt)];
+    };
+    // The DMA is issued by inline asm: the compiler does not track it, so it does not wait for it
+    // before every LDS read of the current buffer (it cannot tell the two buffers apart); the
+    // batch loop waits for it explicitly (vmcnt(0) before the batch barrier).
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)s_lds;
+    auto issue = [&](uint32_t gid, int buf) {
+#pragma unroll
+        for (int k = 0; k < NCP; ++k) {
+            if ((k & 3) != w) continue;  // wave-uniform
+            const int q = min(2 * k + (l >> 5), RF4 - 1);
+            const float4* src = a.records + (size_t)gid * RF4 + q;
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)((buf * SBUF + 2 * k * NB) * 16));
+            int keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+        }
+    };
+
+    int r = 0;
+    if (max_last > 0) issue(batch_gid(max_last), 0);
+    uint32_t gid_next = max_last > NB ? batch_gid(max_last - NB) : 0u;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int buf = 0;
+#ifdef R3DG_EXP_COUNT
+    const long long t_begin = wall_clock64();
+    long long t_wait = 0, t_mask = 0;
+#endif
+    for (int hi = max_last; hi > 0; hi -= NB) {
+        const int cnt = min(NB, hi);
+        const int hn = hi - NB;
+#ifdef R3DG_EXP_COUNT
+        const long long tm0 = wall_clock64();
+#endif
+        if (hn > 0) {  // block-uniform: stage the next batch while this one blends
+            issue(gid_next, buf ^ 1);
+            gid_next = hn > NB ? batch_gid(hn - NB) : 0u;
+        }
+        st = s_lds + buf * SBUF;
+        // this wave's live instances: the cull for its own quadrant, evaluated by lanes 0..cnt-1
+        uint32_t slot_l = 0u;
+        bool mine = false;
+        if (l < cnt) {
+            const float4 co = st[l], r1 = st[NB + l];
+            slot_l = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
+            mine = quadrant_live(make_float2(r1.x, r1.y), co, qx0, qy0, a.cull);
+        }
+        uint32_t bits = (uint32_t)__ballot(mine);
+        const int lo = hi - wmax;  // instances j < lo lie beyond every pixel of this wave
+        if (lo >= 32) bits = 0u;
+        else if (lo > 0) bits &= ~0u << lo;
+#ifdef R3DG_EXP_COUNT
+        if (l == 0) R3DG_EXP_ADD(0, __builtin_popcount(bits));
+        t_mask += wall_clock64() - tm0;
+#endif
+        auto rec0 = [&](int j) { return st[__builtin_amdgcn_readfirstlane(j)]; };
+        auto pos = [&](int j) {
+            return *reinterpret_cast<const float2*>(st + NB + __builtin_amdgcn_readfirstlane(j));
+        };
+        while (bits) {
+            const int j0 = __builtin_ctz(bits);
+            bits &= bits - 1;
+            const bool has1 = bits != 0u;
+            const int j1 = has1 ? __builtin_ctz(bits) : j0;
+            bits &= bits - 1;
+            const float4 co0 = rec0(j0), co1 = rec0(j1);
+            const float2 xy0 = pos(j0), xy1 = pos(j1);
+#if R3DG_BWD_EARLY_ATTR  // both attribute rows read before the power / exp / settle chain
+            float4 va0[NA4], va1[NA4];
+            attrs(j0, va0);
+            attrs(j1, va1);
+#endif
+            const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
+            const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
+            float G0 = fast_expf(pw0), G1 = fast_expf(pw1);
+            settle_threshold2(pw0, co0.w, G0, pw1, co1.w, G1);
+#if !R3DG_BWD_EARLY_ATTR
+            float4 va0[NA4], va1[NA4];
+            attrs(j0, va0);
+            attrs(j1, va1);
+#endif
+            float wv0, qv0, wv1, qv1;
+            step(va0, hi - 1 - j0, true, co0.w, pw0, G0, wv0, qv0);
+            step(va1, hi - 1 - j1, has1, co1.w, pw1, G1, wv1, qv1);
+            float* wr = wq + r * WQS + l;
+            wr[0] = wv0;
+            wr[GRP * WQS] = qv0;
+            wr[WQS] = wv1;
+            wr[(GRP + 1) * WQS] = qv1;
+            rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j0) * 4 + w), r);
+            rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j1) * 4 + w), r + 1);
+            r += has1 ? 2 : 1;
+            if (r > GRP - 2) {
+                flush(r);
+                r = 0;
+            }
+        }
+        // the next batch's records have landed (this wave's DMA) and every wave is done with
+        // this buffer before the next iteration's DMA overwrites it
+#ifdef R3DG_EXP_COUNT
+        const long long tw0 = wall_clock64();
+#endif
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#ifdef R3DG_EXP_COUNT
+        t_wait += wall_clock64() - tw0;
+#endif
+        buf ^= 1;
+    }
+    if (r > 0) flush(r);
+#ifdef R3DG_EXP_COUNT
+    if (l == 0) {
+        R3DG_EXP_ADD(2, t_wait);                    // batch-end DMA wait + barrier, per wave
+        R3DG_EXP_ADD(3, wall_clock64() - t_begin);  // batch loop total, per wave
+        R3DG_EXP_ADD(4, t_mask);                    // DMA issue + cull masks, per wave
+    }
+#endif
+}
+
 template <int SMAX>
 static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
     // R3DG_BWD: "dpp" = DPP-reduction cross-check, "wave" = one 64-thread workgroup per (tile,
-    // quadrant) (measured 7 % slower at M1), default = one 256-thread workgroup per tile
+    // quadrant) (measured 7 % slower at M1), "block" = one 256-thread workgroup per tile with
+    // register staging (2 barriers per batch, measured 2.7 % slower), default = the DMA-staged
+    // workgroup per tile (render_bwd_glds_kernel). All write the same partial rows.
     const char* e = getenv("R3DG_BWD");
     const int grid = padded_tile_grid(a.num_tiles);
     if (e && e[0] == 'd')
         launch_kernel(render_bwd_dpp_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
     else if (e && e[0] == 'w')
         launch_kernel(render_bwd_mfma_kernel<SMAX, true>, dim3(4 * grid), dim3(64), stream, a);
-    else
+    else if (e && e[0] == 'b')
         launch_kernel(render_bwd_mfma_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
+    else
+        launch_kernel(render_bwd_glds_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
     return hipGetLastError();
 }
 

@@ -19,4 +19,5 @@ names = ["bwd live pairs", "bwd mfma groups", "bwd staging wall ticks (sum over 
 for i, n in enumerate(names):
     print(f"{n}: {buf[i]}")
 print(f"bwd staging fraction: {buf[2] / max(buf[3], 1):.3f}")
+print(f"bwd mask/issue ticks: {buf[4]} ({buf[4] / max(buf[3], 1):.3f})")
 print(f"fwd steps done: {fb[2]}\nfwd live pairs (pre-exit): {fb[3]}")

@@ -34,7 +34,7 @@ out = {"config": config, "source": [pmc, cnt],
        "method": "valu_insts = SQ_INSTS_VALU - SQ_INSTS_MFMA per launch (wave instructions); "
                  "evals = live wave-steps x 64 (R3DG_EXP_COUNT build, one M1 step)"}
 steps = {"render_fwd": grab("fwd steps done"), "render_bwd": grab("bwd live pairs")}
-for name, prefix in [("render_fwd", "render_fwd_kernel"), ("render_bwd", "render_bwd_mfma_kernel"),
+for name, prefix in [("render_fwd", "render_fwd_kernel"), ("render_bwd", "render_bwd_glds_kernel"),
                      ("row_sum", "row_sum_kernel")]:
     k, v = pick(prefix)
     ent = {"kernel": k, "valu_insts": int(round(v["SQ_INSTS_VALU"] - v.get("SQ_INSTS_MFMA", 0.0))),
