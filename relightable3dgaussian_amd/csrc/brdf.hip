@@ -51,6 +51,7 @@ struct Sample {
     float local[3], global[3], vis, light[3];
     float hdn, hdo, ndi, ndo, half_norm, half[3];
     float fd[3], fs[3], D, F[3], V;
+    float e_amp, inv_half_norm;  // eval_brdf_fast only
 };
 
 struct GaussBRDF {
@@ -116,7 +117,34 @@ __device__ __forceinline__ void eval_brdf(const GaussBRDF& G, float3 d, Sample& 
     s.V = (0.5f / fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f)) * (0.5f / fmaxf(s.ndo * (1 - r2v) + r2v, 0.0000001f));
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        s.fd[c] = (1 - G.metal) * base[c] / kPi;
+        s.fd[c] = (1 - G.metal) * base[c] * (1.0f / kPi);
+        const float F0 = 0.04f * (1.0f - G.metal) + base[c] * G.metal;
+        s.F[c] = F0 + (1.0f - F0) * p5;
+        s.fs[c] = s.D * s.F[c] * s.V;
+    }
+}
+
+// eval_brdf for the backward: the per-Gaussian terms (amp, sharp, r2v, the view-side GGX factor
+// g2) hoisted by the caller, reciprocal multiplications for the sample's divisions and products
+// for powf(x, 5) (agrees with eval_brdf to ~1e-6 relative; the forward kernels keep eval_brdf).
+__device__ __forceinline__ void eval_brdf_fast(const GaussBRDF& G, float3 d, float amp, float sharp, float r2v,
+                                               float g2, Sample& s) {
+    const float hx = d.x + G.v.x, hy = d.y + G.v.y, hz = d.z + G.v.z;
+    s.half_norm = fmaxf(sqrtf(hx * hx + hy * hy + hz * hz), 0.0000001f);
+    s.inv_half_norm = __builtin_amdgcn_rcpf(s.half_norm);
+    s.half[0] = hx * s.inv_half_norm; s.half[1] = hy * s.inv_half_norm; s.half[2] = hz * s.inv_half_norm;
+    s.hdn = fmaxf(s.half[0] * G.n.x + s.half[1] * G.n.y + s.half[2] * G.n.z, 0.0f);
+    s.hdo = fmaxf(s.half[0] * G.v.x + s.half[1] * G.v.y + s.half[2] * G.v.z, 0.0f);
+    s.ndi = fmaxf(G.n.x * d.x + G.n.y * d.y + G.n.z * d.z, 0.0f);
+    s.ndo = fmaxf(G.n.x * G.v.x + G.n.y * G.v.y + G.n.z * G.v.z, 0.0f);
+    const float base[3] = {G.base.x, G.base.y, G.base.z};
+    s.e_amp = __expf(sharp * (s.hdn - 1.0f));
+    s.D = amp * s.e_amp;
+    const float t1 = 1.0f - s.hdo, t2 = t1 * t1, p5 = t2 * t2 * t1;
+    s.V = (0.5f * __builtin_amdgcn_rcpf(fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f))) * g2;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        s.fd[c] = (1 - G.metal) * base[c] * (1.0f / kPi);
         const float F0 = 0.04f * (1.0f - G.metal) + base[c] * G.metal;
         s.F[c] = F0 + (1.0f - F0) * p5;
         s.fs[c] = s.D * s.F[c] * s.V;
@@ -172,10 +200,21 @@ __global__ void __launch_bounds__(256) brdf_fwd_kernel(BrdfKArgs a) {
     const int Ns = in.sample_num;
     float pbr[3] = {0.f, 0.f, 0.f}, dl[3] = {0.f, 0.f, 0.f}, ldl[3] = {0.f, 0.f, 0.f};
     float rd[3] = {0.f, 0.f, 0.f}, rs[3] = {0.f, 0.f, 0.f};
+    // per-Gaussian BRDF terms (eval_brdf_fast)
+    const float r2 = fmaxf(G.rough * G.rough, 0.0000001f);
+    const float amp = 1.0f / (r2 * kPi), sharp = 2.0f / r2;
+    const float r2v = (1.0f + G.rough) * (1.0f + G.rough) / 8.0f;
+    const float ndo = fmaxf(G.n.x * G.v.x + G.n.y * G.v.y + G.n.z * G.v.z, 0.0f);
+    const float g2 = 0.5f / fmaxf(ndo * (1 - r2v) + r2v, 0.0000001f);
+    const bool rnd = !COMPLEX && a.is_training;
+    float rnext = rnd && Ns > 0 ? a.rand_float[(size_t)idx * Ns] : 0.f;  // one sample ahead
     for (int r = 0; r < Ns; ++r) {
         const size_t w = (size_t)idx * Ns + r;
         float rot = 0.f;
-        if (!COMPLEX && a.is_training) rot = a.rand_float[w] * 2 * kPi;
+        if (rnd) {
+            rot = rnext * 2 * kPi;
+            if (r + 1 < Ns) rnext = a.rand_float[w + 1];
+        }
         const float3 d = fib_dir(G.n, r, Ns, rot);
         float coef[16];
         sh_coef16(d.x, d.y, d.z, coef);
@@ -184,7 +223,7 @@ __global__ void __launch_bounds__(256) brdf_fwd_kernel(BrdfKArgs a) {
             eval_lights<NI, ND, NV>(coef, inc_r, NI, in.direct_shs, ND, vis_r, NV, s);
         else
             eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, in.direct_shs, in.S_direct, vis_g, in.S_visibility, s);
-        eval_brdf(G, d, s);
+        eval_brdf_fast(G, d, amp, sharp, r2v, g2, s);
         const float tmp = 2.0f * kPi * s.ndi / (float)Ns;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -236,15 +275,28 @@ __global__ void __launch_bounds__(256) brdf_fwd_kernel(BrdfKArgs a) {
     }
 }
 
-// render_equation.cu:277-460 (bug-compatible, see header). ND must be > 0 here (register
-// accumulators for the environment-SH gradient); S_direct <= 16 is checked on the host.
+// render_equation.cu:277-460 (bug-compatible, see header); S <= 16 is checked on the host. One
+// thread per Gaussian, samples in the reference's order, the Gaussian's SH coefficients and all
+// 112 SH-gradient accumulators in registers (one wave per SIMD: 256 VGPR + ~50 AGPR). Measured
+// alternatives, all slower at P = 1M: the coefficients staged in LDS at 2 waves/SIMD (spills;
+// 3.9 ms incl. the old reducer), 2 waves/SIMD with registers only (spills, 3.3 ms), the sample
+// loop unrolled by 2 / 3 (accumulators move to AGPRs), the environment SH re-read through the
+// scalar cache each sample (R3DG_BRDF_ENV_RELOAD: no SGPR spills but exposed latency, +0.27 ms).
+// What paid: the next sample's direction loaded one iteration ahead, per-Gaussian BRDF terms
+// hoisted (eval_brdf_fast), reciprocal multiplications instead of divisions, products instead of
+// powf, compile-time loop bounds in the S = 16 specialisation (1051 -> 514 VALU per sample), and
+// a parallel env-gradient reducer (brdf_dir_reduce_kernel): 2.33 -> 0.58 ms in all.
+#ifndef R3DG_BRDF_REG_WAVES
+#define R3DG_BRDF_REG_WAVES 1
+#endif
 template <int NI, int ND, int NV>
-__global__ void __launch_bounds__(256) brdf_bwd_kernel(BrdfKArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R3DG_BRDF_REG_WAVES)))
+brdf_bwd_kernel(BrdfKArgs a) {
     constexpr int NDA = 16;  // register accumulators for dL_ddirect_shs (S_direct <= 16)
     const r3dg_brdf_inputs& in = a.in;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = idx < in.P;
-    const int S_dir = in.S_direct;
+    const int S_dir = ND > 0 ? ND : in.S_direct;  // compile-time bounds in the S = 16 specialisation
     float ddir[3 * NDA];
 #pragma unroll
     for (int i = 0; i < 3 * NDA; ++i) ddir[i] = 0.f;
@@ -271,28 +323,44 @@ __global__ void __launch_bounds__(256) brdf_bwd_kernel(BrdfKArgs a) {
         if (NV == 0) for (int i = 0; i < in.S_visibility; ++i) dvis_g[i] = 0.f;
         float dbase_acc[3] = {0.f, 0.f, 0.f}, dn_acc[3] = {0.f, 0.f, 0.f}, dv_acc[3] = {0.f, 0.f, 0.f};
         float dmetal_acc = 0.f, drough_acc = 0.f;
-        const int n_inc_upd = min(S_dir, in.S_incident);  // reference loop bound is S_direct (:450)
+        const int n_inc_upd = min(S_dir, NI > 0 ? NI : in.S_incident);  // reference loop bound is S_direct (:450)
+        const float rough = G.rough, metal = G.metal;
+        const float r2 = fmaxf(rough * rough, 0.0000001f);
+        const float amp = 1.0f / (r2 * kPi), sharp = 2.0f / r2;
+        const float r2v = (1.0f + rough) * (1.0f + rough) / 8.0f;
+        const float ndo = fmaxf(G.n.x * G.v.x + G.n.y * G.v.y + G.n.z * G.v.z, 0.0f);
+        const float den2 = fmaxf(ndo * (1 - r2v) + r2v, 0.0000001f);
+        const float g2 = 0.5f / den2;
+        const float* dirs = a.dirs_in + (size_t)idx * Ns * 3;
+        float dn0 = Ns > 0 ? dirs[0] : 0.f, dn1 = Ns > 0 ? dirs[1] : 0.f, dn2 = Ns > 0 ? dirs[2] : 0.f;
+#pragma unroll 1  // unrolling by 2 / 3 measured slower (accumulators move to AGPRs)
         for (int r = 0; r < Ns; ++r) {
-            const size_t w = (size_t)idx * Ns + r;
-            const float3 d = make_float3(a.dirs_in[3 * w], a.dirs_in[3 * w + 1], a.dirs_in[3 * w + 2]);
+            const float3 d = make_float3(dn0, dn1, dn2);
+            if (r + 1 < Ns) {  // next sample's direction one iteration ahead
+                dn0 = dirs[3 * r + 3];
+                dn1 = dirs[3 * r + 4];
+                dn2 = dirs[3 * r + 5];
+            }
             const float dd[3] = {d.x, d.y, d.z};
             float coef[16];
             sh_coef16(d.x, d.y, d.z, coef);
             Sample s;
+            // R3DG_BRDF_ENV_RELOAD: the environment SH pointer laundered per sample, so its 48
+            // values are re-read through the scalar cache instead of held in SGPRs (no SGPR spills,
+            // but the reloads' latency shows at one wave per SIMD: measured slower)
+            const float* env = in.direct_shs;
+#ifdef R3DG_BRDF_ENV_RELOAD
+            asm volatile("" : "+s"(env));
+#endif
             if constexpr (NI > 0)
-                eval_lights<NI, ND, NV>(coef, inc_r, NI, in.direct_shs, ND, vis_r, NV, s);
+                eval_lights<NI, ND, NV>(coef, inc_r, NI, env, ND, vis_r, NV, s);
             else
-                eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, in.direct_shs, S_dir, vis_g, in.S_visibility, s);
-            eval_brdf(G, d, s);
-            const float rough = G.rough, metal = G.metal;
-            const float r2 = fmaxf(rough * rough, 0.0000001f);
-            const float amp = 1.0f / (r2 * kPi), sharp = 2.0f / r2;
-            const float e_amp = expf(sharp * (s.hdn - 1.0f));
-            const float r2v = powf(1.0f + rough, 2.0f) / 8.0f;
+                eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, env, S_dir, vis_g, in.S_visibility, s);
+            eval_brdf_fast(G, d, amp, sharp, r2v, g2, s);
+            const float e_amp = s.e_amp;
             const float den1 = fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f);
-            const float den2 = fmaxf(s.ndo * (1 - r2v) + r2v, 0.0000001f);
-            const float g1 = 0.5f / den1, g2 = 0.5f / den2;
-            const float Tn = 2.0f * kPi * s.ndi / (float)Ns;
+            const float g1 = 0.5f * __builtin_amdgcn_rcpf(den1);
+            const float Tn = s.ndi * K;
             float dfd[3], dfs[3], dli[3], fsum[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -309,8 +377,8 @@ __global__ void __launch_bounds__(256) brdf_bwd_kernel(BrdfKArgs a) {
             (void)dndi;  // overwritten below, as in the reference (:403)
             float dbase[3];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) dbase[c] = dfd[c] * (1 - metal) / kPi;
-            float dmetal = -(dfd[0] * b[0] + dfd[1] * b[1] + dfd[2] * b[2]) / kPi;
+            for (int c = 0; c < 3; ++c) dbase[c] = dfd[c] * ((1 - metal) * (1.0f / kPi));
+            float dmetal = -(dfd[0] * b[0] + dfd[1] * b[1] + dfd[2] * b[2]) * (1.0f / kPi);
             const float dD = dfs[0] * s.V * s.F[0] + dfs[1] * s.V * s.F[1] + dfs[2] * s.V * s.F[2];
             float dF[3];
 #pragma unroll
@@ -321,7 +389,7 @@ __global__ void __launch_bounds__(256) brdf_bwd_kernel(BrdfKArgs a) {
             const float dhdn = sharp * e_amp * de;
             const float dr2 = -2.0f / (r2 * r2) * dsharp - 1.0f / (r2 * r2 * kPi) * damp;
             float drough = dr2 * 2.0f * rough;
-            const float p5 = powf(1.0f - s.hdo, 5.0f), p4 = powf(1.0f - s.hdo, 4.0f);
+            const float t1 = 1.0f - s.hdo, t2 = t1 * t1, p4 = t2 * t2, p5 = p4 * t1;
             float dF0[3], dhdo = 0.f;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -334,7 +402,7 @@ __global__ void __launch_bounds__(256) brdf_bwd_kernel(BrdfKArgs a) {
             for (int c = 0; c < 3; ++c) dbase[c] += metal * dF0[c];
             dmetal += (b[0] - 0.04f) * dF0[0] + (b[1] - 0.04f) * dF0[1] + (b[2] - 0.04f) * dF0[2];
             const float dg1 = dV * g2, dg2 = dV * g1;
-            const float dden1 = -0.5f / (den1 * den1) * dg1, dden2 = -0.5f / (den2 * den2) * dg2;
+            const float dden1 = -2.0f * (g1 * g1) * dg1, dden2 = -2.0f * (g2 * g2) * dg2;
             const float dndi2 = dden1 * (1 - r2v);
             const float dndo = dden2 * (1 - r2v);
             const float dr2v = (1.0f - s.ndi) * dden1 + (1.0f - s.ndo) * dden2;
@@ -357,7 +425,7 @@ __global__ void __launch_bounds__(256) brdf_bwd_kernel(BrdfKArgs a) {
                 for (int c = 0; c < 3; ++c) { dn[c] += v[c] * dndo; dv[c] += n[c] * dndo; }
             }
 #pragma unroll
-            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] / s.half_norm;
+            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] * s.inv_half_norm;
             float dglob[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) dglob[c] = dli[c] * s.vis;
@@ -428,12 +496,24 @@ __global__ void __launch_bounds__(256) brdf_bwd_kernel(BrdfKArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(64) brdf_dir_reduce_kernel(const float* partials, int nblocks, int n, float* out) {
-    const int i = threadIdx.x;
-    if (i >= n) return;
+// Sum of the block partials of dL_ddirect_shs: one workgroup per output, a strided per-thread sum
+// (fixed order) then a fixed-shape tree over the workgroup -- deterministic. (The first version
+// ran one thread per output over all block partials in sequence: 1.27 ms at P = 1M, more than
+// the backward kernel itself.)
+__global__ void __launch_bounds__(256) brdf_dir_reduce_kernel(const float* partials, int nblocks, int n, float* out) {
+    const int i = blockIdx.x, t = threadIdx.x;
+    if (i >= n) return;  // workgroup-uniform
     float s = 0.f;
-    for (int b = 0; b < nblocks; ++b) s += partials[(size_t)b * 48 + i];
-    out[i] = s;
+    for (int b = t; b < nblocks; b += 256) s += partials[(size_t)b * 48 + i];
+    __shared__ float s_red[256];
+    s_red[t] = s;
+    __syncthreads();
+#pragma unroll
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h) s_red[t] += s_red[t + h];
+        __syncthreads();
+    }
+    if (t == 0) out[i] = s_red[0];
 }
 
 template <bool COMPLEX>
@@ -518,8 +598,8 @@ extern "C" int r3dg_render_equation_backward(const r3dg_brdf_inputs* in, const f
     else
         hipLaunchKernelGGL((brdf_bwd_kernel<0, 0, 0>), dim3(nb), dim3(256), 0, st, a);
     R3DG_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(brdf_dir_reduce_kernel, dim3(1), dim3(64), 0, st, partials, nb, 3 * in->S_direct,
-                       out->dL_ddirect_shs);
+    hipLaunchKernelGGL(brdf_dir_reduce_kernel, dim3(max(1, 3 * in->S_direct)), dim3(256), 0, st, partials, nb,
+                       3 * in->S_direct, out->dL_ddirect_shs);
     R3DG_CHECK_HIP(hipGetLastError());
     return R3DG_OK;
 }
