@@ -249,9 +249,6 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
-#ifndef R3DG_BWD_EARLY_ATTR
-#define R3DG_BWD_EARLY_ATTR 0  // glds kernel: a pair's attribute rows read before its exp (measured: no gain)
-#endif
 #ifndef R3DG_BWDW_NB
 #define R3DG_BWDW_NB 32  // instances staged per batch by a one-wave workgroup
 #endif
@@ -644,17 +641,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     const float4* st = s_lds;  // staging buffer of the current batch
     const float qx0 = (float)(tx * kTileX + (w & 1) * 8), qy0 = (float)(ty * kTileY + (w >> 1) * 8);
 
-    auto attrs = [&](int j, float4* v4) {
-        const int ju = __builtin_amdgcn_readfirstlane(j);
-#pragma unroll
-        for (int q = 0; q < NA4; ++q) v4[q] = st[(2 + q) * NB + ju];
-    };
-    auto step = [&](const float4* v4, int p, bool live, float opacity, float power, float G, float& wv, float& qv) {
+    auto step = [&](int j, int p, bool live, float opacity, float power, float G, float& wv, float& qv) {
 #pragma clang fp contract(off)
+        const int ju = __builtin_amdgcn_readfirstlane(j);
         float v[NA4 * 4];
 #pragma unroll
         for (int q = 0; q < NA4; ++q) {
-            const float4 rr = v4[q];
+            const float4 rr = st[(2 + q) * NB + ju];
             v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
         }
         const float alpha = fminf(0.99f, opacity * G);
@@ -789,23 +782,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             bits &= bits - 1;
             const float4 co0 = rec0(j0), co1 = rec0(j1);
             const float2 xy0 = pos(j0), xy1 = pos(j1);
-#if R3DG_BWD_EARLY_ATTR  // both attribute rows read before the power / exp / settle chain
-            float4 va0[NA4], va1[NA4];
-            attrs(j0, va0);
-            attrs(j1, va1);
-#endif
             const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
             const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
             float G0 = fast_expf(pw0), G1 = fast_expf(pw1);
             settle_threshold2(pw0, co0.w, G0, pw1, co1.w, G1);
-#if !R3DG_BWD_EARLY_ATTR
-            float4 va0[NA4], va1[NA4];
-            attrs(j0, va0);
-            attrs(j1, va1);
-#endif
             float wv0, qv0, wv1, qv1;
-            step(va0, hi - 1 - j0, true, co0.w, pw0, G0, wv0, qv0);
-            step(va1, hi - 1 - j1, has1, co1.w, pw1, G1, wv1, qv1);
+            step(j0, hi - 1 - j0, true, co0.w, pw0, G0, wv0, qv0);
+            step(j1, hi - 1 - j1, has1, co1.w, pw1, G1, wv1, qv1);
             float* wr = wq + r * WQS + l;
             wr[0] = wv0;
             wr[GRP * WQS] = qv0;

@@ -33,7 +33,9 @@ def pick(prefix):
 out = {"config": config, "source": [pmc, cnt],
        "method": "valu_insts = SQ_INSTS_VALU - SQ_INSTS_MFMA per launch (wave instructions); "
                  "evals = live wave-steps x 64 (R3DG_EXP_COUNT build, one M1 step)"}
-steps = {"render_fwd": grab("fwd steps done"), "render_bwd": grab("bwd live pairs")}
+runs = grab("m1 steps run") or 1  # the counters add up over every M1 step the counting run made
+steps = {k: (v // runs if v else v) for k, v in
+         {"render_fwd": grab("fwd steps done"), "render_bwd": grab("bwd live pairs")}.items()}
 for name, prefix in [("render_fwd", "render_fwd_kernel"), ("render_bwd", "render_bwd_glds_kernel"),
                      ("row_sum", "row_sum_kernel")]:
     k, v = pick(prefix)
