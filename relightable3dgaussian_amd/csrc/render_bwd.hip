@@ -249,6 +249,9 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
+#ifndef R3DG_BWDG_PWNB
+#define R3DG_BWDG_PWNB 16  // instances per staged batch of the per-wave DMA variant
+#endif
 #ifndef R3DG_BWDW_NB
 #define R3DG_BWDW_NB 32  // instances staged per batch by a one-wave workgroup
 #endif
@@ -572,30 +575,45 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
 // [q * NB + t], two columns per DMA wave-instruction (lanes 0-31 column 2k, lanes 32-63 column
 // 2k+1). Same blend step, MFMA flush and partial rows as render_bwd_mfma_kernel.
 // ---------------------------------------------------------------------------------------------
-template <int SMAX>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
+// PW = true: one 64-thread workgroup per (tile, quadrant) with its own (smaller) staging double
+// buffer: no block barriers, and a wave stages only up to its own n_contrib maximum.
+template <int SMAX, bool PW>
+__global__ void __launch_bounds__(PW ? 64 : kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
 render_bwd_glds_kernel(RenderBwdArgs a) {
-    constexpr int NB = 32;                        // instances per batch (two batches staged)
+    constexpr int NB = PW ? R3DG_BWDG_PWNB : 32;  // instances per batch (two batches staged)
+    constexpr int NW = PW ? 1 : 4;                // waves per workgroup
     constexpr int NA4 = (4 + SMAX + 3) / 4;
     constexpr int NXB = (4 + SMAX + 15) / 16;
     constexpr int XW = 16 * NXB;
     constexpr int GRP = 16;
     constexpr int RF4 = 2 + NA4;                  // float4s per render record
-    constexpr int NCP = (RF4 + 1) / 2;            // DMA wave-instructions per batch
-    constexpr int SBUF = 2 * NCP * NB;            // float4s per staging buffer
+    constexpr int NCP = (RF4 * NB + 63) / 64;     // DMA wave-instructions per batch
+    constexpr int SBUF = RF4 * NB;                // float4s per staging buffer
     constexpr int WQF4 = 2 * GRP * WQS / 4;       // float4s per wave's w|q image
     static_assert((2 * GRP * WQS) % 4 == 0, "w|q image must be float4-sized");
+    static_assert(64 % NB == 0, "a DMA wave-instruction covers whole columns");
     // one LDS array (a second __shared__ object can make the compiler wait for the DMA before
-    // unrelated LDS reads): [2 staging buffers | 4 w|q images | max_last]
-    __shared__ float4 s_lds[2 * SBUF + 4 * WQF4 + 1];
+    // unrelated LDS reads): [2 staging buffers | w|q images | max_last]
+    __shared__ float4 s_lds[2 * SBUF + NW * WQF4 + 1];
 
-    const int tile = block_tile(a.tile_order, a.num_tiles);
+    int tile, w;
+    if constexpr (PW) {
+        // the four quadrant workgroups of a tile are blocks b, b+8, b+16, b+24: one XCD
+        const int b = blockIdx.x, xcd = b & 7, k = b >> 3;
+        w = k & 3;
+        const int vb = ((k >> 2) << 3) | xcd;
+        tile = a.tile_order ? (vb < a.num_tiles ? (int)a.tile_order[vb] : a.num_tiles)
+                            : xcd_tile(vb, (int)gridDim.x >> 2);
+    } else {
+        tile = block_tile(a.tile_order, a.num_tiles);
+        w = threadIdx.x >> 6;
+    }
     if (tile >= a.num_tiles) return;
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int t = threadIdx.x, l = t & 63;
     R3DG_BWD_PIXELS()
     float T = T_final;
-    float* wq = reinterpret_cast<float*>(s_lds + 2 * SBUF + w * WQF4);
-    int* s_max_last = reinterpret_cast<int*>(s_lds + 2 * SBUF + 4 * WQF4);
+    float* wq = reinterpret_cast<float*>(s_lds + 2 * SBUF + (PW ? 0 : w) * WQF4);
+    int* s_max_last = reinterpret_cast<int*>(s_lds + 2 * SBUF + NW * WQF4);
 
     float bX[NXB][16];
     {
@@ -635,7 +653,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     const float TFB = T_final * bg_dot;
     int rowj = 0;
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
-    const int max_last = block_max_last(wmax, s_max_last);
+    const int max_last = PW ? wmax : block_max_last(wmax, s_max_last);
     const int RS = a.RS;
     const int nch = l & 15;
     const float4* st = s_lds;  // staging buffer of the current batch
@@ -713,7 +731,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     // Gaussian of instance (l & 31) of the batch ending at tile position hi_b (tail lanes clamp
     // to the batch's last instance, so every DMA lane reads a valid record)
     auto batch_gid = [&](int hi_b) -> uint32_t {
-        const int tt = min(l & 31, min(NB, hi_b) - 1);
+        const int tt = min(l & (NB - 1), min(NB, hi_b) - 1);
         return a.point_list[range.x + (uint32_t)(hi_b - 1 - tt)];
     };
     // The DMA is issued by inline asm: the compiler does not track it, so it does not wait for it
@@ -723,13 +741,16 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     auto issue = [&](uint32_t gid, int buf) {
 #pragma unroll
         for (int k = 0; k < NCP; ++k) {
-            if ((k & 3) != w) continue;  // wave-uniform
-            const int q = min(2 * k + (l >> 5), RF4 - 1);
-            const float4* src = a.records + (size_t)gid * RF4 + q;
-            const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)((buf * SBUF + 2 * k * NB) * 16));
-            int keep;
-            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                         : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+            if (!PW && (k & 3) != w) continue;  // wave-uniform
+            // lane l of instruction k: entry k * 64 + l = column q, instance l % NB
+            const int q = (k * 64 + l) / NB;
+            const float4* src = a.records + (size_t)gid * RF4 + min(q, RF4 - 1);
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)((buf * SBUF + k * 64) * 16));
+            if (q < RF4) {  // lanes past the last column are masked off (they would write past the buffer)
+                int keep;
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                             : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+            }
         }
     };
 
@@ -737,7 +758,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     if (max_last > 0) issue(batch_gid(max_last), 0);
     uint32_t gid_next = max_last > NB ? batch_gid(max_last - NB) : 0u;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (PW) wave_lds_sync();
+    else __syncthreads();
     int buf = 0;
 #ifdef R3DG_EXP_COUNT
     const long long t_begin = wall_clock64();
@@ -808,7 +830,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         const long long tw0 = wall_clock64();
 #endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if constexpr (PW) wave_lds_sync();
+        else __syncthreads();
 #ifdef R3DG_EXP_COUNT
         t_wait += wall_clock64() - tw0;
 #endif
@@ -838,8 +861,10 @@ static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
         launch_kernel(render_bwd_mfma_kernel<SMAX, true>, dim3(4 * grid), dim3(64), stream, a);
     else if (e && e[0] == 'b')
         launch_kernel(render_bwd_mfma_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
+    else if (e && e[0] == 'q')
+        launch_kernel(render_bwd_glds_kernel<SMAX, true>, dim3(4 * grid), dim3(64), stream, a);
     else
-        launch_kernel(render_bwd_glds_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
+        launch_kernel(render_bwd_glds_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
     return hipGetLastError();
 }
 

@@ -452,7 +452,7 @@ def test_backward_mfma_matches_dpp_variant(hip_ext, S):
     h = hip_forward(hip_ext, scene, cam, S=S)
     dc, do, dd, df = upstream_grads(cam.height, cam.width, S)
     gm = hip_backward(hip_ext, h, dc, do, dd, df)
-    for variant in ("dpp", "wave", "block"):  # DPP reductions; one-wave-per-quadrant workgroups; register staging
+    for variant in ("dpp", "wave", "block", "quad"):  # DPP reductions; per-quadrant workgroups; register staging; per-quadrant DMA
         os.environ["R3DG_BWD"] = variant
         try:
             gd = hip_backward(hip_ext, h, dc, do, dd, df)
