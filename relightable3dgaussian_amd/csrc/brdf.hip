@@ -516,9 +516,134 @@ __global__ void __launch_bounds__(256) brdf_dir_reduce_kernel(const float* parti
     if (t == 0) out[i] = s_red[0];
 }
 
+// Lane-per-sample forward (render_equation.cu:552-663 training / :52-187 complex): a workgroup
+// of 256 lanes holds GB = 256 / Ns whole Gaussians, lane t = (Gaussian t / Ns, sample t % Ns).
+// A lane's per-sample outputs sit at w = g * Ns + r = g0 * Ns + t, so every per-sample store of
+// the workgroup is one contiguous span (the thread-per-Gaussian kernel stores at a 288-byte lane
+// stride, Ns * 3 floats, and spent most of its time there). The per-Gaussian sums over the
+// samples run in the reference's order (r = 0, 1, ...) from an LDS column per output channel, so
+// they are the thread-per-Gaussian kernel's sums bit for bit.
+template <int NI, int ND, int NV, bool COMPLEX>
+__global__ void __launch_bounds__(256) brdf_fwd_lane_kernel(BrdfKArgs a, int GB) {
+    constexpr int NC = COMPLEX ? 12 : 6;  // per-Gaussian sums: complex dl ldl rd rs, else pbr dl
+    __shared__ float s_c[256 * (NC + 1)];
+    __shared__ float s_sum[256][NC];
+    const r3dg_brdf_inputs& in = a.in;
+    const int Ns = in.sample_num;
+    const int t = threadIdx.x;
+    const int gl = t / Ns, r = t - gl * Ns;
+    const int g0 = blockIdx.x * GB;
+    const int ng = min(GB, in.P - g0);
+    const bool active = gl < ng;
+    float c[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) c[k] = 0.f;
+    if (active) {
+        const int idx = g0 + gl;
+        GaussBRDF G;
+        float inc_r[NI > 0 ? 3 * NI : 1], vis_r[NV > 0 ? NV : 1];
+        load_gauss<NI, ND, NV>(in, idx, G, inc_r, vis_r);
+        const float* inc_g = in.incidents_shs + (size_t)idx * 3 * in.S_incident;
+        const float* vis_g = in.visibility_shs + (size_t)idx * in.S_visibility;
+        const float r2 = fmaxf(G.rough * G.rough, 0.0000001f);
+        const float amp = 1.0f / (r2 * kPi), sharp = 2.0f / r2;
+        const float r2v = (1.0f + G.rough) * (1.0f + G.rough) / 8.0f;
+        const float ndo = fmaxf(G.n.x * G.v.x + G.n.y * G.v.y + G.n.z * G.v.z, 0.0f);
+        const float g2 = 0.5f / fmaxf(ndo * (1 - r2v) + r2v, 0.0000001f);
+        const size_t w = (size_t)idx * Ns + r;
+        float rot = 0.f;
+        if (!COMPLEX && a.is_training) rot = a.rand_float[w] * 2 * kPi;
+        const float3 d = fib_dir(G.n, r, Ns, rot);
+        float coef[16];
+        sh_coef16(d.x, d.y, d.z, coef);
+        Sample s;
+        if constexpr (NI > 0)
+            eval_lights<NI, ND, NV>(coef, inc_r, NI, in.direct_shs, ND, vis_r, NV, s);
+        else
+            eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, in.direct_shs, in.S_direct, vis_g, in.S_visibility, s);
+        eval_brdf_fast(G, d, amp, sharp, r2v, g2, s);
+        const float tmp = 2.0f * kPi * s.ndi / (float)Ns;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float tr = s.light[k] * tmp;
+            if constexpr (COMPLEX) {
+                c[k] = tr;
+                c[3 + k] = s.local[k] * tmp;
+                c[6 + k] = s.fd[k] * tr;
+                c[9 + k] = s.fs[k] * tr;
+            } else {
+                c[k] = (s.fd[k] + s.fs[k]) * tr;
+                c[3 + k] = tr;
+            }
+        }
+        if constexpr (COMPLEX) {
+            const r3dg_brdf_complex_outputs& o = a.cx;
+            o.incident_dirs[3 * w] = d.x; o.incident_dirs[3 * w + 1] = d.y; o.incident_dirs[3 * w + 2] = d.z;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                o.incident_lights[3 * w + k] = s.light[k];
+                o.local_incident_lights[3 * w + k] = s.local[k];
+                o.global_incident_lights[3 * w + k] = s.vis * s.global[k];
+            }
+            o.incident_visibility[w] = s.vis;
+        } else {
+            a.incident_dirs[3 * w] = d.x; a.incident_dirs[3 * w + 1] = d.y; a.incident_dirs[3 * w + 2] = d.z;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NC; ++k) s_c[t * (NC + 1) + k] = c[k];
+    __syncthreads();
+    // per (Gaussian, channel): the samples' contributions summed in sample order (the reference's
+    // per-thread accumulation, render_equation.cu:630-655)
+    for (int e = t; e < ng * NC; e += 256) {
+        const int gg = e / NC, k = e - gg * NC;
+        float acc = 0.f;
+        for (int rr = 0; rr < Ns; ++rr) acc += s_c[(gg * Ns + rr) * (NC + 1) + k];
+        s_sum[gg][k] = acc;
+    }
+    __syncthreads();
+    if (t < ng) {
+        const int idx = g0 + t;
+        const float* v = s_sum[t];
+        if constexpr (COMPLEX) {
+            const r3dg_brdf_complex_outputs& o = a.cx;
+            float av[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) av[k] = v[k] / kPi + v[9 + k];
+            o.accum[idx] = (av[0] + av[1] + av[2]) / 3;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                o.pbr[3 * idx + k] = v[6 + k] + v[9 + k];
+                o.rgb_d[3 * idx + k] = v[6 + k];
+                o.rgb_s[3 * idx + k] = v[9 + k];
+                o.diffuse_light[3 * idx + k] = v[k];
+                o.local_diffuse_light[3 * idx + k] = v[3 + k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                a.pbr[3 * idx + k] = v[k];
+                a.diffuse[3 * idx + k] = v[3 + k];
+            }
+        }
+    }
+}
+
 template <bool COMPLEX>
 static hipError_t launch_fwd(const BrdfKArgs& a, hipStream_t st) {
     const r3dg_brdf_inputs& in = a.in;
+    const bool s16 = in.S_incident == 16 && in.S_direct == 16 && in.S_visibility == 16;
+    const int Ns = in.sample_num;
+    const char* e = getenv("R3DG_BRDF_FWD");  // "thread": the thread-per-Gaussian kernel
+    if (Ns >= 1 && Ns <= 256 && !(e && e[0] == 't')) {
+        const int GB = 256 / Ns;
+        const dim3 grid((in.P + GB - 1) / GB), block(256);
+        if (s16)
+            hipLaunchKernelGGL((brdf_fwd_lane_kernel<16, 16, 16, COMPLEX>), grid, block, 0, st, a, GB);
+        else
+            hipLaunchKernelGGL((brdf_fwd_lane_kernel<0, 0, 0, COMPLEX>), grid, block, 0, st, a, GB);
+        return hipGetLastError();
+    }
     const dim3 grid((in.P + 255) / 256), block(256);
     if (in.S_incident == 16 && in.S_direct == 16 && in.S_visibility == 16)
         hipLaunchKernelGGL((brdf_fwd_kernel<16, 16, 16, COMPLEX>), grid, block, 0, st, a);
