@@ -126,13 +126,15 @@ __device__ __forceinline__ void eval_brdf(const GaussBRDF& G, float3 d, Sample& 
 
 // eval_brdf for the backward: the per-Gaussian terms (amp, sharp, r2v, the view-side GGX factor
 // g2) hoisted by the caller, reciprocal multiplications for the sample's divisions and products
-// for powf(x, 5) (agrees with eval_brdf to ~1e-6 relative; the forward kernels keep eval_brdf).
+// for powf(x, 5) (agrees with eval_brdf to ~1e-6 relative).
 __device__ __forceinline__ void eval_brdf_fast(const GaussBRDF& G, float3 d, float amp, float sharp, float r2v,
                                                float g2, Sample& s) {
     const float hx = d.x + G.v.x, hy = d.y + G.v.y, hz = d.z + G.v.z;
     s.half_norm = fmaxf(sqrtf(hx * hx + hy * hy + hz * hz), 0.0000001f);
+    // the half vector by true divisions, as eval_brdf: the sharp specular lobe (sharp = 2 / r^2,
+    // 800 at roughness 0.05) amplifies an ulp of h.n into 1e-4 of the roughness gradient
     s.inv_half_norm = __builtin_amdgcn_rcpf(s.half_norm);
-    s.half[0] = hx * s.inv_half_norm; s.half[1] = hy * s.inv_half_norm; s.half[2] = hz * s.inv_half_norm;
+    s.half[0] = hx / s.half_norm; s.half[1] = hy / s.half_norm; s.half[2] = hz / s.half_norm;
     s.hdn = fmaxf(s.half[0] * G.n.x + s.half[1] * G.n.y + s.half[2] * G.n.z, 0.0f);
     s.hdo = fmaxf(s.half[0] * G.v.x + s.half[1] * G.v.y + s.half[2] * G.v.z, 0.0f);
     s.ndi = fmaxf(G.n.x * d.x + G.n.y * d.y + G.n.z * d.z, 0.0f);

@@ -51,3 +51,33 @@ def test_c2_s21_full_frame_parity(hip_ext):
     scene = synthetic.ball_scene(300_000, S=21, seed=0)
     o = _full_check(hip_ext, scene, cam, 21, (1.0, 1.0, 1.0))
     assert o["num_rendered"] > 300_000
+
+
+def test_c3_training_step_full_size(hip_ext):
+    """C3 (hotdog training stand-in) at full size: 250k Gaussians, 800x800, S = 11, black
+    background -- raster forward + backward against the oracle on the whole frame, then the
+    training-mode BRDF (random rotations passed in) forward and backward on all 250k Gaussians."""
+    from tests._helpers import tt
+    from tests.test_gpu_parity import _brdf_tensors
+
+    cam = synthetic.orbit_camera(30.0, 20.0, 4.0311, 0.6911112, 800, 800)
+    scene = synthetic.ball_scene(250_000, S=11, seed=2)
+    o = _full_check(hip_ext, scene, cam, 11, (0.0, 0.0, 0.0))
+    assert o["num_rendered"] > 250_000
+    P = 250_000
+    inp = synthetic.brdf_inputs(P, seed=7)
+    rnd = np.random.default_rng(8).uniform(0, 1, (P, 24, 1)).astype(np.float32)
+    pbr, dirs, dl = hip_ext.render_equation_forward_with_rand(*_brdf_tensors(inp), 24, True, tt(rnd))
+    of = oracle.brdf_forward(inp, 24, True, rnd)
+    # same bars as test_brdf_training_forward_with_rand (fma-contracted rotation angle)
+    for k, v in zip(["pbr", "incident_dirs", "diffuse_light"], (pbr, dirs, dl)):
+        assert_close(k, v.cpu().numpy(), of[k], 2e-4, 1e-3)
+    rng = np.random.default_rng(9)
+    gp = rng.normal(size=(P, 3)).astype(np.float32)
+    gd = rng.normal(size=(P, 3)).astype(np.float32)
+    out = hip_ext.render_equation_backward(*_brdf_tensors(inp), 24, tt(of["incident_dirs"]), tt(gp), tt(gd), False)
+    ob = oracle.brdf_backward(inp, of["incident_dirs"], gp, gd, 24)
+    for k, v in zip(["base", "rough", "metal", "normals", "viewdirs", "incidents", "env", "visibility"], out):
+        ref = ob[k]
+        tol = (5e-4 if k == "env" else 2e-5) * max(float(np.abs(ref).max()), 1e-9)
+        assert_close("d_" + k, v.cpu().numpy(), ref, tol, 1e-3)
