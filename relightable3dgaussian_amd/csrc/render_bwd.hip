@@ -249,6 +249,13 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
+#ifndef R3DG_BWDG_NB
+#define R3DG_BWDG_NB 64  // instances per staged batch of the DMA-staged kernel
+#endif
+#ifndef R3DG_BWDG_GRP
+#define R3DG_BWDG_GRP 12  // instances per MFMA group of the DMA-staged kernel (64 / 12 measured best of
+                          // 32 / 16, 64 / 12, 32 / 12: the smaller w|q image buys the larger batch)
+#endif
 #ifndef R3DG_BWDG_PWNB
 #define R3DG_BWDG_PWNB 16  // instances per staged batch of the per-wave DMA variant
 #endif
@@ -580,21 +587,26 @@ render_bwd_mfma_kernel(RenderBwdArgs a) {
 template <int SMAX, bool PW>
 __global__ void __launch_bounds__(PW ? 64 : kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
 render_bwd_glds_kernel(RenderBwdArgs a) {
-    constexpr int NB = PW ? R3DG_BWDG_PWNB : 32;  // instances per batch (two batches staged)
+    constexpr int NB = PW ? R3DG_BWDG_PWNB : R3DG_BWDG_NB;  // instances per batch (two batches staged)
     constexpr int NW = PW ? 1 : 4;                // waves per workgroup
     constexpr int NA4 = (4 + SMAX + 3) / 4;
     constexpr int NXB = (4 + SMAX + 15) / 16;
     constexpr int XW = 16 * NXB;
-    constexpr int GRP = 16;
+    constexpr int GRP = R3DG_BWDG_GRP;            // instances per MFMA group (<= 16 A rows)
     constexpr int RF4 = 2 + NA4;                  // float4s per render record
     constexpr int NCP = (RF4 * NB + 63) / 64;     // DMA wave-instructions per batch
     constexpr int SBUF = RF4 * NB;                // float4s per staging buffer
     constexpr int WQF4 = 2 * GRP * WQS / 4;       // float4s per wave's w|q image
     static_assert((2 * GRP * WQS) % 4 == 0, "w|q image must be float4-sized");
-    static_assert(64 % NB == 0, "a DMA wave-instruction covers whole columns");
+    static_assert(64 % NB == 0 || NB % 64 == 0, "a DMA wave-instruction covers whole columns");
+    static_assert(NB <= 64 && GRP <= 16, "live masks are one ballot; MFMA groups are 16 rows");
+    using mask_t = typename std::conditional<(NB > 32), unsigned long long, uint32_t>::type;
     // one LDS array (a second __shared__ object can make the compiler wait for the DMA before
-    // unrelated LDS reads): [2 staging buffers | w|q images | max_last]
-    __shared__ float4 s_lds[2 * SBUF + NW * WQF4 + 1];
+    // unrelated LDS reads): [w|q images | 2 staging buffers | max_last]. With GRP < 16 the MFMA's
+    // A reads of rows GRP..15 run past a wave's image into the next image or the staging buffer
+    // (valid LDS, values ignored: those D rows are never stored).
+    __shared__ float4 s_lds[NW * WQF4 + 2 * SBUF + 1];
+    float4* const stage = s_lds + NW * WQF4;
 
     int tile, w;
     if constexpr (PW) {
@@ -612,8 +624,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     const int t = threadIdx.x, l = t & 63;
     R3DG_BWD_PIXELS()
     float T = T_final;
-    float* wq = reinterpret_cast<float*>(s_lds + 2 * SBUF + (PW ? 0 : w) * WQF4);
-    int* s_max_last = reinterpret_cast<int*>(s_lds + 2 * SBUF + NW * WQF4);
+    float* wq = reinterpret_cast<float*>(s_lds + (PW ? 0 : w) * WQF4);
+    int* s_max_last = reinterpret_cast<int*>(stage + 2 * SBUF);
 
     float bX[NXB][16];
     {
@@ -656,7 +668,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     const int max_last = PW ? wmax : block_max_last(wmax, s_max_last);
     const int RS = a.RS;
     const int nch = l & 15;
-    const float4* st = s_lds;  // staging buffer of the current batch
+    const float4* st = stage;  // staging buffer of the current batch
     const float qx0 = (float)(tx * kTileX + (w & 1) * 8), qy0 = (float)(ty * kTileY + (w >> 1) * 8);
 
     auto step = [&](int j, int p, bool live, float opacity, float power, float G, float& wv, float& qv) {
@@ -745,7 +757,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             // lane l of instruction k: entry k * 64 + l = column q, instance l % NB
             const int q = (k * 64 + l) / NB;
             const float4* src = a.records + (size_t)gid * RF4 + min(q, RF4 - 1);
-            const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)((buf * SBUF + k * 64) * 16));
+            const uint32_t dst =
+                __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)((NW * WQF4 + buf * SBUF + k * 64) * 16));
             if (q < RF4) {  // lanes past the last column are masked off (they would write past the buffer)
                 int keep;
                 asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -775,7 +788,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             issue(gid_next, buf ^ 1);
             gid_next = hn > NB ? batch_gid(hn - NB) : 0u;
         }
-        st = s_lds + buf * SBUF;
+        st = stage + buf * SBUF;
         // this wave's live instances: the cull for its own quadrant, evaluated by lanes 0..cnt-1
         uint32_t slot_l = 0u;
         bool mine = false;
@@ -784,12 +797,12 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             slot_l = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
             mine = quadrant_live(make_float2(r1.x, r1.y), co, qx0, qy0, a.cull);
         }
-        uint32_t bits = (uint32_t)__ballot(mine);
+        mask_t bits = (mask_t)__ballot(mine);
         const int lo = hi - wmax;  // instances j < lo lie beyond every pixel of this wave
-        if (lo >= 32) bits = 0u;
-        else if (lo > 0) bits &= ~0u << lo;
+        if (lo >= NB) bits = 0u;
+        else if (lo > 0) bits &= ~(mask_t)0 << lo;
 #ifdef R3DG_EXP_COUNT
-        if (l == 0) R3DG_EXP_ADD(0, __builtin_popcount(bits));
+        if (l == 0) R3DG_EXP_ADD(0, __builtin_popcountll(bits));
         t_mask += wall_clock64() - tm0;
 #endif
         auto rec0 = [&](int j) { return st[__builtin_amdgcn_readfirstlane(j)]; };
@@ -797,10 +810,10 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             return *reinterpret_cast<const float2*>(st + NB + __builtin_amdgcn_readfirstlane(j));
         };
         while (bits) {
-            const int j0 = __builtin_ctz(bits);
+            const int j0 = (int)__builtin_ctzll(bits);
             bits &= bits - 1;
             const bool has1 = bits != 0u;
-            const int j1 = has1 ? __builtin_ctz(bits) : j0;
+            const int j1 = has1 ? (int)__builtin_ctzll(bits) : j0;
             bits &= bits - 1;
             const float4 co0 = rec0(j0), co1 = rec0(j1);
             const float2 xy0 = pos(j0), xy1 = pos(j1);
