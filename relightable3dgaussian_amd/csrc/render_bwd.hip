@@ -249,6 +249,9 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
+#ifndef R3DG_BWD_SKIP_EMPTY
+#define R3DG_BWD_SKIP_EMPTY 1  // DMA-staged kernel: instances no pixel of the wave blended get no row
+#endif
 #ifndef R3DG_BWDG_NB
 #define R3DG_BWDG_NB 64  // instances per staged batch of the DMA-staged kernel
 #endif
@@ -671,7 +674,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     const float4* st = stage;  // staging buffer of the current batch
     const float qx0 = (float)(tx * kTileX + (w & 1) * 8), qy0 = (float)(ty * kTileY + (w >> 1) * 8);
 
-    auto step = [&](int j, int p, bool live, float opacity, float power, float G, float& wv, float& qv) {
+    auto step = [&](int j, int p, bool live, float opacity, float power, float G, float& wv, float& qv,
+                    bool& okv) {
 #pragma clang fp contract(off)
         const int ju = __builtin_amdgcn_readfirstlane(j);
         float v[NA4 * 4];
@@ -682,6 +686,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         }
         const float alpha = fminf(0.99f, opacity * G);
         const bool ok = live && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+        okv = ok;
         const float ae = ok ? alpha : 0.f;
         const float Ge = ok ? G : 0.f;
         const float rinv = __builtin_amdgcn_rcpf(1.f - ae);
@@ -822,16 +827,31 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             float G0 = fast_expf(pw0), G1 = fast_expf(pw1);
             settle_threshold2(pw0, co0.w, G0, pw1, co1.w, G1);
             float wv0, qv0, wv1, qv1;
-            step(j0, hi - 1 - j0, true, co0.w, pw0, G0, wv0, qv0);
-            step(j1, hi - 1 - j1, has1, co1.w, pw1, G1, wv1, qv1);
-            float* wr = wq + r * WQS + l;
-            wr[0] = wv0;
-            wr[GRP * WQS] = qv0;
-            wr[WQS] = wv1;
-            wr[(GRP + 1) * WQS] = qv1;
-            rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j0) * 4 + w), r);
-            rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j1) * 4 + w), r + 1);
-            r += has1 ? 2 : 1;
+            bool ok0, ok1;
+            step(j0, hi - 1 - j0, true, co0.w, pw0, G0, wv0, qv0, ok0);
+            step(j1, hi - 1 - j1, has1, co1.w, pw1, G1, wv1, qv1, ok1);
+            // an instance no pixel of this wave blended (the cull is conservative; pixels may sit
+            // past their n_contrib) has w = q = 0 on every lane: it joins no MFMA group and gets no
+            // partial row (its flag stays 0; the row-sum adds nothing for it either way)
+#if R3DG_BWD_SKIP_EMPTY
+            const bool any0 = __ballot(ok0) != 0ull, any1 = __ballot(ok1) != 0ull;
+#else
+            const bool any0 = true, any1 = has1;
+#endif
+            if (any0) {
+                float* wr = wq + r * WQS + l;
+                wr[0] = wv0;
+                wr[GRP * WQS] = qv0;
+                rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j0) * 4 + w), r);
+            }
+            const int r1 = r + (any0 ? 1 : 0);
+            if (any1) {
+                float* wr = wq + r1 * WQS + l;
+                wr[0] = wv1;
+                wr[GRP * WQS] = qv1;
+                rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j1) * 4 + w), r1);
+            }
+            r = r1 + (any1 ? 1 : 0);
             if (r > GRP - 2) {
                 flush(r);
                 r = 0;
