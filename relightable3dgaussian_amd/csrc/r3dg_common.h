@@ -280,6 +280,15 @@ __device__ __forceinline__ float qform_min_rect(float a, float b, float c, float
     return fminf(fminf(edge_x(xa), edge_x(xb)), fminf(edge_y(ya), edge_y(yb)));
 }
 
+// Cull margin on the threshold t = 2 ln(255 o) of Q = -2 power: t (1 + m) + m. The fp32 error of
+// the blend's power (two FMAs over terms bounded by 2 lambda_max d^2, so ~1e-6 kappa relative for a
+// conic of condition kappa), of exp (<= 2 ulp) and of the minimiser below are orders of magnitude
+// under m = 0.01 for any conic the preprocess produces (tests/test_gpu_parity.py: cull on == off
+// bit for bit, anisotropic scales included). Round 1 used m = 0.1.
+#ifndef R3DG_CULL_MARGIN
+#define R3DG_CULL_MARGIN 0.01f
+#endif
+
 // quadrant_mask's test for one quadrant with top-left pixel (qx, qy): may alpha reach 1/255 there
 // (bit q of quadrant_mask(xy, co, x0, y0, cull) for qx = x0 + (q & 1) * 8, qy = y0 + (q >> 1) * 8).
 __device__ __forceinline__ bool quadrant_live(float2 xy, float4 co, float qx, float qy, int cull) {
@@ -287,7 +296,7 @@ __device__ __forceinline__ bool quadrant_live(float2 xy, float4 co, float qx, fl
     if (co.w < 1.0f / 255.0f) return false;
     const float det = co.x * co.z - co.y * co.y;
     if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return true;
-    const float t = 2.0f * __logf(255.0f * co.w) * 1.1f + 0.1f;
+    const float t = 2.0f * __logf(255.0f * co.w) * (1.0f + R3DG_CULL_MARGIN) + R3DG_CULL_MARGIN;
     if (!(t < 1e30f)) return true;
     const float ia = __builtin_amdgcn_rcpf(co.x), ic = __builtin_amdgcn_rcpf(co.z);
     return !(qform_min_rect(co.x, co.y, co.z, ia, ic, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f) > t);
@@ -295,15 +304,15 @@ __device__ __forceinline__ bool quadrant_live(float2 xy, float4 co, float qx, fl
 
 // Conservative set of the 8x8 quadrants of tile (x0, y0) in which alpha = o exp(-Q/2) can reach
 // 1/255, i.e. Q <= 2 ln(255 o). A quadrant is dropped only if the minimum of Q over its pixel
-// rectangle exceeds t = 2 ln(255 o) * 1.1 + 0.1 -- the 10 % + 0.1 margin covers the fp32
-// rounding of the blend's power and of __expf, so a dropped instance fails the reference's
-// alpha test on every pixel of the quadrant (tests/test_gpu_parity.py: cull on == off bitwise).
+// rectangle exceeds t = 2 ln(255 o) (1 + m) + m (R3DG_CULL_MARGIN), so a dropped instance fails
+// the reference's alpha test on every pixel of the quadrant (tests/test_gpu_parity.py: cull on ==
+// off bitwise).
 __device__ __forceinline__ uint32_t quadrant_mask(float2 xy, float4 co, int x0, int y0, int cull) {
     if (!cull) return 0xFu;
     if (co.w < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 everywhere
     const float det = co.x * co.z - co.y * co.y;
     if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return 0xFu;
-    const float t = 2.0f * __logf(255.0f * co.w) * 1.1f + 0.1f;
+    const float t = 2.0f * __logf(255.0f * co.w) * (1.0f + R3DG_CULL_MARGIN) + R3DG_CULL_MARGIN;
     if (!(t < 1e30f)) return 0xFu;
     // approximate reciprocals: an inexact minimiser changes Q only at second order
     const float ia = __builtin_amdgcn_rcpf(co.x), ic = __builtin_amdgcn_rcpf(co.z);
