@@ -751,6 +751,8 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     // scratch: partial rows [4L, RS] (one per instance and quadrant, written sparsely) and the
     // per-Gaussian sums [P, RS]; the rows' presence flags live in the binning state, zeroed by the
     // forward's duplicate pass (a row's presence depends on the forward state only)
+    // the backward blend addresses partial rows with 32-bit element offsets
+    R3DG_REQUIRE((size_t)RS * 4 * (size_t)L < (1ull << 31), "rasterize_gaussians_backward: too many tile instances");
     const size_t row_bytes = sizeof(float) * (size_t)RS * 4 * L;
     const size_t sum_bytes = sizeof(float) * (size_t)RS * P;
     char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + sum_bytes);

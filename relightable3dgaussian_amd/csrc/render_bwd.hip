@@ -735,7 +735,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             const int row = (l >> 4) * 4 + i;
             const uint32_t base = (uint32_t)__shfl(rowj, row);
             if (row < r) {
-                float* dst = a.rows + (size_t)base * RS;
+                // 32-bit element offset: 4L rows x RS floats stay below 2^31 (checked on the host)
+                float* dst = a.rows + (uint32_t)(base * (uint32_t)RS);
 #pragma unroll
                 for (int xb = 0; xb < NXB; ++xb) dst[xb * 16 + nch] = accX[xb][i];
                 if (nch < 6) dst[XW + nch] = accY[i];
