@@ -256,8 +256,8 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
 #define R3DG_BWDG_NB 64  // instances per staged batch of the DMA-staged kernel
 #endif
 #ifndef R3DG_BWDG_GRP
-#define R3DG_BWDG_GRP 12  // instances per MFMA group of the DMA-staged kernel (64 / 12 measured best of
-                          // 32 / 16, 64 / 12, 32 / 12: the smaller w|q image buys the larger batch)
+#define R3DG_BWDG_GRP 13  // instances per MFMA group of the DMA-staged kernel (64 / 13 measured best of
+                          // 32 / 16, 64 / 12, 64 / 13, 32 / 12: the smaller w|q image buys the larger batch)
 #endif
 #ifndef R3DG_BWDG_PWNB
 #define R3DG_BWDG_PWNB 16  // instances per staged batch of the per-wave DMA variant
