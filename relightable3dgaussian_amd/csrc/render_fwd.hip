@@ -15,6 +15,9 @@
 //     instances with s_ff1 -- no per-instance scalar test;
 //   * early exit per wave (ballot) and per block (__syncthreads_count), as the reference;
 //   * XCD-aware tile order (r3dg_kernels.h).
+// Default-shader path: render_fwd_glds_kernel stages the render records of the next 64-instance
+// batch by LDS-DMA while the current one blends (one barrier per batch, 8 waves/SIMD; M1 forward
+// 0.484 -> 0.447 ms); render_fwd_kernel stays for the splat shaders and as R3DG_FWD=ld.
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
 
@@ -259,13 +262,194 @@ render_fwd_kernel(RenderFwdArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Double-buffered variant of the default-shader blend (render records only): the records of batch
+// b+1 are copied HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no staging stores)
+// while the waves blend batch b, so the record round trip leaves the critical path and a batch
+// costs one block barrier (the early-exit count) instead of two. Every wave evaluates the exact
+// quadrant cull of the staged instances for its own quadrant (render_bwd_glds_kernel does the
+// same). Staging layout: column q (float4 q of the render record) of instance j at [q * NB + j].
+// Same blend step, same decisions and sums as render_fwd_kernel (bitwise).
+// ---------------------------------------------------------------------------------------------
+#ifndef R3DG_FWDG_NB
+#define R3DG_FWDG_NB 64  // instances per staged batch (two resident: 12.3 KB, 64 VGPRs -> 8 waves/SIMD;
+                         // 128: 24.6 KB -> 6 waves/SIMD, measured 0.480 vs 0.447 ms at M1)
+#endif
+
+template <int SMAX>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_FWD_WAVES : 1)))
+render_fwd_glds_kernel(RenderFwdArgs a) {
+    constexpr int NB = R3DG_FWDG_NB;
+    constexpr int NH = NB / 64;                // staged instances per lane
+    constexpr int NA4 = (4 + SMAX + 3) / 4;    // float4 per attribute row
+    constexpr int RF4 = 2 + NA4;               // float4 per render record
+    constexpr int SBUF = RF4 * NB;             // float4 per staging buffer
+    constexpr int NCP = RF4 * NH;              // DMA wave-instructions per batch
+    static_assert(NB % 64 == 0 && NB <= 256, "a DMA wave-instruction covers 64 instances of one column");
+    __shared__ float4 s_lds[2 * SBUF];
+
+    const int tile = block_tile(a.tile_order, a.num_tiles);
+    if (tile >= a.num_tiles) return;
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
+    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const float pfx = (float)px, pfy = (float)py;
+    const float qx0 = (float)(tx * kTileX + (w & 1) * 8), qy0 = (float)(ty * kTileY + (w >> 1) * 8);
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+
+    bool done = !inside;
+    float T = 1.0f;
+    uint32_t last = 0;
+    float C[3] = {0.f, 0.f, 0.f}, F[SMAX > 0 ? SMAX : 1];
+    float Dp = 0.f, Op = 0.f;
+#pragma unroll
+    for (int c = 0; c < SMAX; ++c) F[c] = 0.f;
+
+    // Gaussian of staged instance h * 64 + l of the batch at tile position b0 (tail lanes clamp to
+    // the tile's last instance, so every DMA lane reads a valid record)
+    auto load_gids = [&](int b0, uint32_t (&gd)[NH]) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) gd[h] = a.point_list[range.x + (uint32_t)min(b0 + h * 64 + l, n - 1)];
+    };
+    // the DMA is inline asm: the compiler does not wait for it before the LDS reads of the other
+    // buffer; the batch loop waits for it explicitly (vmcnt(0) before the batch barrier)
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)s_lds;
+    auto issue = [&](const uint32_t (&gd)[NH], int buf) {
+#pragma unroll
+        for (int k = 0; k < NCP; ++k) {
+            if ((k & 3) != w) continue;  // wave-uniform
+            // lane l of instruction k: column k / NH, instance (k % NH) * 64 + l -> entry k * 64 + l
+            const float4* src = a.records + (size_t)gd[k % NH] * RF4 + k / NH;
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)((buf * SBUF + k * 64) * 16));
+            int keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+        }
+    };
+
+    uint32_t gnext[NH];
+    if (n > 0) {
+        uint32_t g0[NH];
+        load_gids(0, g0);
+        issue(g0, 0);
+        if (n > NB) load_gids(NB, gnext);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int buf = 0;
+    for (int base = 0; base < n; base += NB) {
+        // batch `base` has landed (every wave waited for its own DMA) and nobody reads the other
+        // buffer any more
+        if (__syncthreads_count(done) == kBlock) break;
+        if (base + NB < n) {  // block-uniform: stage the next batch while this one blends
+            issue(gnext, buf ^ 1);
+            if (base + 2 * NB < n) load_gids(base + 2 * NB, gnext);
+        }
+        const float4* st = s_lds + buf * SBUF;
+        const int cnt = min(NB, n - base);
+        unsigned long long bits[NH];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const int j = h * 64 + l;
+            bool mine = false;
+            if (j < cnt) {
+                const float4 co = st[j], r1 = st[NB + j];
+                mine = quadrant_live(make_float2(r1.x, r1.y), co, qx0, qy0, a.cull);
+            }
+            bits[h] = __ballot(mine);
+        }
+        auto step = [&](int j, bool live, float opacity, float power, float G) {
+#pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
+            const int ju = __builtin_amdgcn_readfirstlane(j);
+            float v[NA4 * 4];
+#pragma unroll
+            for (int q = 0; q < NA4; ++q) {
+                const float4 r = st[(2 + q) * NB + ju];
+                v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
+            }
+            const float alpha = fminf(0.99f, opacity * G);  // bit-identical to the oracle
+            const bool contrib = live && !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const float test_T = T * (1.0f - alpha);
+            const bool stop = test_T < 0.0001f;
+            done = done || (contrib && stop);
+            if (contrib && !stop) {
+                const float wgt = alpha * T;
+                C[0] = __builtin_fmaf(v[0], wgt, C[0]);
+                C[1] = __builtin_fmaf(v[1], wgt, C[1]);
+                C[2] = __builtin_fmaf(v[2], wgt, C[2]);
+#pragma unroll
+                for (int c2 = 0; c2 < SMAX; ++c2) F[c2] = __builtin_fmaf(v[4 + c2], wgt, F[c2]);
+                Dp = __builtin_fmaf(v[3], wgt, Dp);
+                Op += wgt;
+                T = test_T;
+                last = (uint32_t)(base + j + 1);
+            }
+        };
+        bool alive = __ballot(!done) != 0ull;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            unsigned long long b = bits[h];
+            while (alive && b) {
+                const int j0 = h * 64 + (int)__builtin_ctzll(b);
+                b &= b - 1;
+                const bool has1 = b != 0ull;
+                const int j1 = has1 ? h * 64 + (int)__builtin_ctzll(b) : j0;
+                b &= b - 1;
+                const int u0 = __builtin_amdgcn_readfirstlane(j0), u1 = __builtin_amdgcn_readfirstlane(j1);
+                const float4 co0 = st[u0], co1 = st[u1];
+                const float2 xy0 = *reinterpret_cast<const float2*>(st + NB + u0);
+                const float2 xy1 = *reinterpret_cast<const float2*>(st + NB + u1);
+                const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
+                const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
+                const f32x2 G = r3dg_expf2(pw0, pw1);
+                step(j0, true, co0.w, pw0, G.x);
+                step(j1, has1, co1.w, pw1, G.y);
+                if (__ballot(!done) == 0ull) alive = false;  // converged here: a uniform exit
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        buf ^= 1;
+    }
+    // a block that stops early has no DMA in flight: every issued batch was waited for above
+
+    if (inside) {
+        const int pix = py * a.W + px;
+        a.final_T[pix] = T;
+        a.n_contrib[pix] = last;
+        const float b0 = a.bg[0], b1 = a.bg[1], b2 = a.bg[2];
+        const float o0 = C[0] + T * b0, o1 = C[1] + T * b1, o2 = C[2] + T * b2;
+        a.out_color[3 * pix + 0] = o0;
+        a.out_color[3 * pix + 1] = o1;
+        a.out_color[3 * pix + 2] = o2;
+        // default splat shader: shader colour == SH colour (splatShader.cu:67-71)
+        a.out_shader_color[3 * pix + 0] = o0;
+        a.out_shader_color[3 * pix + 1] = o1;
+        a.out_shader_color[3 * pix + 2] = o2;
+        a.out_depth[pix] = Dp;
+        a.out_opacity[pix] = Op;
+        if (a.zero_stencil) a.zero_stencil[pix] = 0.f;
+#pragma unroll
+        for (int c = 0; c < SMAX; ++c)
+            if (c < a.S) a.out_feature[a.flay.a[c] + pix * a.flay.m[c]] = F[c];
+    }
+}
+
 template <int SMAX>
 static hipError_t launch_fwd_s(const RenderFwdArgs& a, bool shader, hipStream_t stream) {
+    // R3DG_FWD=ld: the register-staged kernel for the default shader too (cross-check / A-B)
+    static const bool use_ld = [] {
+        const char* e = getenv("R3DG_FWD");
+        return e && e[0] == 'l';
+    }();
     const int grid = padded_tile_grid(a.num_tiles);
     if (shader)
         launch_kernel(render_fwd_kernel<SMAX, true>, dim3(grid), dim3(kBlock), stream, a);
-    else
+    else if (use_ld || !a.records)
         launch_kernel(render_fwd_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
+    else
+        launch_kernel(render_fwd_glds_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
     return hipGetLastError();
 }
 
