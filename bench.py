@@ -12,8 +12,8 @@ renders its own camera of the same scene (weak scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Rank 0 prints one JSON line. `roofline` prices renderCUDA fwd + bwd -- render_fwd_kernel,
-render_bwd_mfma_kernel and row_sum_kernel (the backward's per-instance reduction) -- with SURVEY.md
+Rank 0 prints one JSON line. `roofline` prices renderCUDA fwd + bwd -- render_fwd_glds_kernel,
+render_bwd_glds_kernel and row_sum_kernel (the backward's per-instance reduction) -- with SURVEY.md
 §8d's algorithmic bytes (272*L + 156*H*W + 16*tiles at S=11) over their device time, from HIP
 events recorded inside each launch's dispatch on the launch stream during K further steps (the
 timed K steps run without events);
@@ -364,7 +364,7 @@ def main() -> None:
         "views_per_s": round(world * args.steps / elapsed, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "renderCUDA fwd + bwd: render_fwd_kernel + render_bwd_glds_kernel + row_sum_kernel",
+                     "kernel": "renderCUDA fwd + bwd: render_fwd_glds_kernel + render_bwd_glds_kernel + row_sum_kernel",
                      "algorithmic_bytes": bf + bb, "kernel_ms": round(t_kern * 1e3, 4), "valu": valu},
         "kernel_ms": {k: round(v, 4) for k, v in avg.items() if prof[k][0]},
     }

@@ -391,6 +391,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
             unsigned long long b = bits[h];
+            if (l == 0) R3DG_EXP_ADD(3, __builtin_popcountll(b));
             while (alive && b) {
                 const int j0 = h * 64 + (int)__builtin_ctzll(b);
                 b &= b - 1;
@@ -406,6 +407,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 const f32x2 G = r3dg_expf2(pw0, pw1);
                 step(j0, true, co0.w, pw0, G.x);
                 step(j1, has1, co1.w, pw1, G.y);
+                if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
                 if (__ballot(!done) == 0ull) alive = false;  // converged here: a uniform exit
             }
         }

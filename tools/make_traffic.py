@@ -19,7 +19,7 @@ def pick(prefix):
 
 
 out = {"config": config, "source": src, "method": "FETCH_SIZE*2 + WRITE_SIZE (KiB*1024), mean per launch"}
-for name, prefix in [("render_fwd", "render_fwd_kernel"), ("render_bwd", "render_bwd_glds_kernel"),
+for name, prefix in [("render_fwd", "render_fwd_glds_kernel"), ("render_bwd", "render_bwd_glds_kernel"),
                      ("row_sum", "row_sum_kernel"), ("gather_bwd", "gather_bwd_kernel"),
                      ("preprocess", "preprocess_kernel")]:
     k, v = pick(prefix)

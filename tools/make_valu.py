@@ -36,7 +36,7 @@ out = {"config": config, "source": [pmc, cnt],
 runs = grab("m1 steps run") or 1  # the counters add up over every M1 step the counting run made
 steps = {k: (v // runs if v else v) for k, v in
          {"render_fwd": grab("fwd steps done"), "render_bwd": grab("bwd live pairs")}.items()}
-for name, prefix in [("render_fwd", "render_fwd_kernel"), ("render_bwd", "render_bwd_glds_kernel"),
+for name, prefix in [("render_fwd", "render_fwd_glds_kernel"), ("render_bwd", "render_bwd_glds_kernel"),
                      ("row_sum", "row_sum_kernel")]:
     k, v = pick(prefix)
     ent = {"kernel": k, "valu_insts": int(round(v["SQ_INSTS_VALU"] - v.get("SQ_INSTS_MFMA", 0.0))),
