@@ -12,6 +12,10 @@
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
 
+#ifndef R3DG_SORT_LONG_IPT
+#define R3DG_SORT_LONG_IPT 8  // items per thread of the depth sort for tiles longer than 1024 instances
+#endif
+
 namespace r3dg {
 
 // forward.cu:25-76.  Writes rgb and the clamp bits.
@@ -319,21 +323,57 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(int T, const uint2* __
 // The depth half of the reference's (tile << 32 | depth bits) sort: every tile's instances,
 // ascending Gaussian ids after the stable tile sort, sorted stably by the Gaussians' depth bits
 // (the reference's order: depth, ties by Gaussian id). One workgroup per tile, longest tiles
-// first. A tile of up to kSortChunk instances is sorted in registers / LDS (rocPRIM block radix
-// sort, 4 passes of 8 bits); a longer one sorts each chunk into a run and merges run pairs
-// (stable merge path) through the scratch buffers, ping-pong, landing in point_list.
-constexpr int kSortIPT = 4;
-constexpr int kSortChunk = 256 * kSortIPT;
-using TileDepthSort = rocprim::block_radix_sort<uint32_t, 256, kSortIPT, uint32_t>;
+// first. A chunk of the tile is sorted in registers / LDS (rocPRIM block radix sort, 4 passes of
+// 8 bits) -- 1024-instance chunks for tiles of up to 1024 instances, 2048-instance chunks for
+// longer ones (both sorters share one LDS union: 16 KB, still 8 waves/SIMD); a tile longer than
+// one chunk sorts each chunk into a run and merges run pairs (stable merge path) through the
+// scratch buffers, ping-pong, landing in point_list.
+constexpr int kSortBT = 256;
+using TileDepthSort4 = rocprim::block_radix_sort<uint32_t, kSortBT, 4, uint32_t>;
+using TileDepthSortL = rocprim::block_radix_sort<uint32_t, kSortBT, R3DG_SORT_LONG_IPT, uint32_t>;
+union TileDepthSortStorage {
+    typename TileDepthSort4::storage_type s4;
+    typename TileDepthSortL::storage_type sl;
+};
 
 __device__ __forceinline__ uint32_t nt_load(const uint32_t* p) { return __builtin_nontemporal_load(p); }
 
-__global__ void __launch_bounds__(256) tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges,
-                                                              const uint32_t* __restrict__ order,
-                                                              const uint32_t* __restrict__ depth_keys,
-                                                              uint32_t* __restrict__ point_list, uint32_t* kA,
-                                                              uint32_t* vA, uint32_t* kB) {
-    __shared__ typename TileDepthSort::storage_type storage;
+// chunks of kSortBT * IPT instances of the tile [s, s + n) sorted into runs at (rk, rv)
+template <int IPT, class Sort, class Storage>
+__device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_t nchunks, const uint32_t* depth_keys,
+                                                 const uint32_t* point_list, uint32_t* rk, uint32_t* rv,
+                                                 Storage& storage) {
+    constexpr uint32_t kChunk = kSortBT * IPT;
+    const int t = threadIdx.x;
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        const uint32_t c0 = c * kChunk;
+        uint32_t keys[IPT], vals[IPT];
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {  // blocked arrangement: item index = t * IPT + k
+            const uint32_t i = c0 + (uint32_t)(t * IPT + k);
+            const uint32_t g = i < n ? point_list[s + i] : 0xffffffffu;
+            vals[k] = g;
+            keys[k] = i < n ? depth_keys[g] : 0xffffffffu;  // visible depths < 0x7f800000: pads sort last
+        }
+        if (c > 0) __syncthreads();  // storage reuse
+        Sort().sort(keys, vals, storage, 0, 32);
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const uint32_t i = c0 + (uint32_t)(t * IPT + k);
+            if (i < n) {
+                if (nchunks > 1) rk[s + i] = keys[k];
+                rv[s + i] = vals[k];
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kSortBT) __attribute__((amdgpu_waves_per_eu(8))) tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges,
+                                                                  const uint32_t* __restrict__ order,
+                                                                  const uint32_t* __restrict__ depth_keys,
+                                                                  uint32_t* __restrict__ point_list, uint32_t* kA,
+                                                                  uint32_t* vA, uint32_t* kB) {
+    __shared__ TileDepthSortStorage storage;
     const int b = blockIdx.x;
     if (b >= T) return;
     const int tile = order ? (int)order[b] : b;
@@ -341,41 +381,23 @@ __global__ void __launch_bounds__(256) tile_depth_sort_kernel(int T, const uint2
     const uint32_t s = rg.x, n = rg.y - rg.x;
     if (n <= 1) return;
     const int t = threadIdx.x;
-    const uint32_t nchunks = (n + kSortChunk - 1) / kSortChunk;
+    const uint32_t kChunk = n <= kSortBT * 4 ? kSortBT * 4 : kSortBT * R3DG_SORT_LONG_IPT;  // block-uniform
+    const uint32_t nchunks = (n + kChunk - 1) / kChunk;
     int rounds = 0;
     while ((1u << rounds) < nchunks) ++rounds;
     // runs go where an even number of merge rounds leaves the result in (kB, point_list)
     uint32_t* rk = (rounds & 1) ? kA : kB;
     uint32_t* rv = (rounds & 1) ? vA : point_list;
-    for (uint32_t c = 0; c < nchunks; ++c) {
-        const uint32_t c0 = c * kSortChunk;
-        uint32_t keys[kSortIPT], vals[kSortIPT];
-#pragma unroll
-        for (int k = 0; k < kSortIPT; ++k) {  // blocked arrangement: item index = t * IPT + k
-            const uint32_t i = c0 + (uint32_t)(t * kSortIPT + k);
-            const uint32_t g = i < n ? point_list[s + i] : 0xffffffffu;
-            vals[k] = g;
-            keys[k] = i < n ? depth_keys[g] : 0xffffffffu;  // visible depths < 0x7f800000: pads sort last
-        }
-        if (c > 0) __syncthreads();  // storage reuse
-        TileDepthSort().sort(keys, vals, storage, 0, 32);
-#pragma unroll
-        for (int k = 0; k < kSortIPT; ++k) {
-            const uint32_t i = c0 + (uint32_t)(t * kSortIPT + k);
-            if (i < n) {
-                if (nchunks > 1) rk[s + i] = keys[k];
-                rv[s + i] = vals[k];
-            }
-        }
-    }
+    if (kChunk == kSortBT * 4) sort_tile_chunks<4, TileDepthSort4>(s, n, nchunks, depth_keys, point_list, rk, rv, storage.s4);
+    else sort_tile_chunks<R3DG_SORT_LONG_IPT, TileDepthSortL>(s, n, nchunks, depth_keys, point_list, rk, rv, storage.sl);
     if (nchunks == 1) return;
     __syncthreads();
     uint32_t *sk = rk, *sv = rv, *dk = (rk == kA) ? kB : kA, *dv = (rk == kA) ? point_list : vA;
-    for (uint32_t w = kSortChunk; w < n; w *= 2) {
+    for (uint32_t w = kChunk; w < n; w *= 2) {
         for (uint32_t a0 = 0; a0 < n; a0 += 2 * w) {
             const uint32_t a1 = min(a0 + w, n), b1 = min(a0 + 2 * w, n);
             const uint32_t la = a1 - a0, lb = b1 - a1, tot = b1 - a0;
-            const uint32_t per = (tot + 255) / 256;
+            const uint32_t per = (tot + kSortBT - 1) / kSortBT;
             const uint32_t d0 = min((uint32_t)t * per, tot), d1 = min(d0 + per, tot);
             if (d0 >= d1) continue;
             const uint32_t* A = sk + s + a0;
@@ -408,6 +430,13 @@ __global__ void __launch_bounds__(256) tile_depth_sort_kernel(int T, const uint2
         uint32_t* tk = sk; sk = dk; dk = tk;
         uint32_t* tv = sv; sv = dv; dv = tv;
     }
+}
+
+hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint32_t* depth_keys,
+                                  uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB, hipStream_t st) {
+    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(T), dim3(kSortBT), 0, st, T, ranges, order, depth_keys, point_list,
+                       kA, vA, kB);
+    return hipGetLastError();
 }
 
 }  // namespace r3dg

@@ -163,8 +163,8 @@ __global__ void duplicate_kernel(int P, const uint32_t* offsets, const float2* m
                                  int grid_y, uint32_t* tile_keys, uint32_t* gid_out, uint32_t* flags, float4* records,
                                  int rec4);
 __global__ void tile_ranges_kernel(int T, int L, const uint32_t* tiles, uint2* ranges);
-__global__ void tile_depth_sort_kernel(int T, const uint2* ranges, const uint32_t* order, const uint32_t* depth_keys,
-                                       uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB);
+hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint32_t* depth_keys,
+                                  uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB, hipStream_t st);
 
 // Slot of an instance from its Gaussian's render record word 1 (x, y, slot0, radius) and its tile.
 __device__ __forceinline__ uint32_t record_slot(float4 r1, int tx, int ty, int grid_x, int grid_y) {

@@ -611,8 +611,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     }
     if (L > 0) {
         ProfScope ps(R3DG_PROF_SORT, st, true);
-        hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(T), dim3(256), 0, st, T, img.ranges, img.tile_order,
-                           geom.depth_keys, bin.point_list, bin.tile_keys, bin.gid_in, bin.keys2);
+        R3DG_CHECK_HIP(launch_tile_depth_sort(T, img.ranges, img.tile_order, geom.depth_keys, bin.point_list,
+                                              bin.tile_keys, bin.gid_in, bin.keys2, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
