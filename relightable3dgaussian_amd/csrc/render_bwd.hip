@@ -1222,15 +1222,20 @@ hipError_t launch_sh_grad_views(int g0, int n, int deg, int M, int N, const floa
 // pixel.x = d0x - x with d0x = mean.x - quadrant centre); c == NXC + 1 sums [Sxy, Syy], the
 // moments whose expansion needs no coefficient. Writes sums + g * RS = [X part (XW) | dL/dmean2D
 // x, y | dL/dconic x, y, z | dL/dopacity | 0, 0] (backward.cu:552-611 summed over the pixels).
+#ifndef R3DG_ROWSUM_PF
+#define R3DG_ROWSUM_PF 1  // row-sum: next chunk's flag word prefetched
+#endif
+
 template <int SMAX>
 __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
     constexpr int NXB = (4 + SMAX + 15) / 16;
     constexpr int NXC = 4 * NXB;                  // float4 columns of a partial row's X part
     constexpr int LPG = NXC + 2 <= 8 ? 8 : 16;    // lanes per Gaussian
     constexpr int CH = 8;                         // slots per chunk (one flag word per lane)
+    constexpr int GPB = 256 / LPG;                // Gaussians per workgroup
     const int RS = a.RS;
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    const int g = a.g_begin + t / LPG, c = t % LPG;
+    const int gb = a.g_begin + blockIdx.x * GPB;  // the workgroup's first Gaussian
+    const int g = gb + (int)threadIdx.x / LPG, c = (int)threadIdx.x % LPG;
     const bool active = g < a.g_end && c < NXC + 2;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     float S0 = 0.f, Sdx = 0.f, Sdy = 0.f, Sdxdx = 0.f, Sdxdy = 0.f, Sdydy = 0.f;
@@ -1246,8 +1251,18 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
         rw = max(x1 - x0, 1);
     }
     const float inv_rw = 1.f / (float)rw;
+#if R3DG_ROWSUM_PF
+    // the next chunk's flag word is loaded before this chunk's rows: one dependent round trip per
+    // chunk instead of two
+    uint32_t fw_next = (c < CH && c < n) ? a.flags[k0 + c] : 0u;
+#endif
     for (uint32_t kb = 0; kb < n; kb += CH) {
+#if R3DG_ROWSUM_PF
+        const uint32_t fw = fw_next;
+        fw_next = (c < CH && kb + CH + c < n) ? a.flags[k0 + kb + CH + c] : 0u;
+#else
         const uint32_t fw = (c < CH && kb + c < n) ? a.flags[k0 + kb + c] : 0u;
+#endif
         uint32_t mask = ((fw & 0xffu) ? 1u : 0u) | ((fw & 0xff00u) ? 2u : 0u) | ((fw & 0xff0000u) ? 4u : 0u) |
                         ((fw & 0xff000000u) ? 8u : 0u);
         mask <<= 4 * (c & (CH - 1));
