@@ -116,6 +116,11 @@ int r3dg_rasterize_gaussians(const r3dg_raster_settings* settings, const r3dg_ga
 
 size_t r3dg_image_state_n_contrib_offset(int H, int W);
 
+/* Bytes of the geometry state buffer for P Gaussians with S features (S < 0: the S-independent
+ * part every per-Gaussian accessor reads, i.e. without the render records). Lets a binding check
+ * a caller-supplied geomBuffer before handing it to r3dg_sh_color_grads. */
+size_t r3dg_geom_state_bytes(int P, int S);
+
 /* Debug / parity accessors into the opaque state buffers (tile keys, sort order, ranges). */
 typedef struct r3dg_binning_view {
     const uint32_t* tile_sorted;  /* [L] tile of each sorted instance; the reference's sort key is

@@ -343,6 +343,19 @@ def expf(x):
     return np.array([f(float(v)) for v in x], np.float32)
 
 
+class blend_exp_libm:
+    """Context manager: the oracle's blend uses glibc expf instead of r3dg_expf (measures the exp
+    choice; the HIP kernels always use r3dg_expf)."""
+
+    def __enter__(self):
+        lib().oracle_set_blend_exp(ctypes.c_int(1))
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_blend_exp(ctypes.c_int(0))
+        return False
+
+
 def expf_accuracy(lo=-80.0, hi=0.0, stride=1):
     """(max ulp error, n, correctly rounded count) of r3dg_expf against double exp over every
     `stride`-th float in [lo, hi]."""

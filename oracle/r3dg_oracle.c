@@ -101,6 +101,14 @@ float r3dg_expf(float x)
     return u2f(f2u(p) + (f2u(kf) << 23));
 }
 
+/* The blend's exp: r3dg_expf (mode 0, what the HIP kernels evaluate) or glibc's expf (mode 1, a
+ * stand-in for a vendor libm exp such as the reference's CUDA expf, forward.cu:477 / backward.cu:527).
+ * Mode 1 exists only to measure how far n_contrib / final_T / the images move when the exp is not
+ * the build's own (tests/test_oracle.py test_blend_exp_choice_c2). */
+static int g_blend_exp_libm = 0;
+void oracle_set_blend_exp(int libm) { g_blend_exp_libm = libm; }
+static float blend_exp(float x) { return g_blend_exp_libm ? expf(x) : r3dg_expf(x); }
+
 /* Accuracy check of r3dg_expf against double-precision exp over the floats x = lo, ... stepping
  * `stride` bit patterns through [lo, hi] (both <= 0): max error in ulp of the float result and the
  * count of correctly rounded results. */
@@ -485,7 +493,7 @@ void oracle_render_forward(int W, int H, int S, const uint32_t* ranges, const ui
                         const float* co = conic_opacity + 4 * id;
                         float power = gauss_power(co, dx, dy);
                         if (power > 0.0f) continue;
-                        float alpha = fminf(0.99f, co[3] * r3dg_expf(power));
+                        float alpha = fminf(0.99f, co[3] * blend_exp(power));
                         if (alpha < 1.0f / 255.0f) continue;
                         float test_T = T * (1 - alpha);
                         if (test_T < 0.0001f) break; /* done = true */
@@ -531,7 +539,7 @@ void oracle_render_intermediate(int W, int H, const uint32_t* ranges, const uint
                         const float* co = conic_opacity + 4 * id;
                         float power = gauss_power(co, dx, dy);
                         if (power > 0.0f) continue;
-                        float G = r3dg_expf(power);
+                        float G = blend_exp(power);
                         float alpha = fminf(0.99f, co[3] * G);
                         float salpha = fminf(0.99f, stencil_opacity[id] * G);
                         if (alpha < 1.0f / 255.0f && salpha < 1.0f / 255.0f) continue;
@@ -635,7 +643,7 @@ void oracle_render_backward(int W, int H, int S, const uint32_t* ranges, const u
                         const float* co = conic_opacity + 4 * id;
                         float power = gauss_power(co, dx, dy);
                         if (power > 0.0f) continue;
-                        float G = r3dg_expf(power);
+                        float G = blend_exp(power);
                         float alpha = fminf(0.99f, co[3] * G);
                         if (alpha < 1.0f / 255.0f) continue;
                         T = T / (1.f - alpha);

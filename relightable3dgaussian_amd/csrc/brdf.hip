@@ -636,8 +636,9 @@ static hipError_t launch_fwd(const BrdfKArgs& a, hipStream_t st) {
     const r3dg_brdf_inputs& in = a.in;
     const bool s16 = in.S_incident == 16 && in.S_direct == 16 && in.S_visibility == 16;
     const int Ns = in.sample_num;
-    const char* e = getenv("R3DG_BRDF_FWD");  // "thread": the thread-per-Gaussian kernel
-    if (Ns >= 1 && Ns <= 256 && !(e && e[0] == 't')) {
+    // a lane per (Gaussian, sample) while a workgroup holds at least one whole Gaussian; beyond 256
+    // samples the thread-per-Gaussian kernel (no call site uses more than 24)
+    if (Ns >= 1 && Ns <= 256) {
         const int GB = 256 / Ns;
         const dim3 grid((in.P + GB - 1) / GB), block(256);
         if (s16)

@@ -111,7 +111,7 @@ __device__ static bool preprocess_one(const PreprocessArgs& a, int idx, const fl
     const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     const float3 pv = xform_point4x3(p, a.view);
     if (pv.z <= 0.2f) {  // auxiliary.h:154 (the reference __trap()s when prefiltered; we flag it)
-        if (a.prefiltered && a.error_flag) atomicOr(a.error_flag, 1u);
+        if (a.prefiltered && a.error_flag) a.error_flag[0] = 1u;  // same value from every writer
         return false;
     }
     const float4 ph = xform_point4x4(p, a.proj);

@@ -74,6 +74,7 @@ struct BinningState {
     uint32_t* point_list;   // [L] Gaussian ids in sorted order (reference point_list)
     uint32_t* keys2;        // [L] depth-sort scratch (tiles longer than one sort chunk)
     uint32_t* flags;        // [L] backward row flags, one byte per (slot, quadrant) (render_bwd.hip)
+    uint8_t* contrib;       // [L] per sorted position: bit q = a pixel of quadrant q blended it (forward)
     void* sort_temp;
     size_t sort_temp_bytes;
 };
@@ -280,14 +281,36 @@ __device__ __forceinline__ float qform_min_rect(float a, float b, float c, float
     return fminf(fminf(edge_x(xa), edge_x(xb)), fminf(edge_y(ya), edge_y(yb)));
 }
 
-// Cull margin on the threshold t = 2 ln(255 o) of Q = -2 power: t (1 + m) + m. The fp32 error of
-// the blend's power (two FMAs over terms bounded by 2 lambda_max d^2, so ~1e-6 kappa relative for a
-// conic of condition kappa), of exp (<= 2 ulp) and of the minimiser below are orders of magnitude
-// under m = 0.01 for any conic the preprocess produces (tests/test_gpu_parity.py: cull on == off
-// bit for bit, anisotropic scales included). Round 1 used m = 0.1.
+// Cull margin on the threshold t = 2 ln(255 o) of Q = -2 power: t (1 + m) + m + e * Mmax.
+// (1 + m) + m (m = 0.01) absorbs the exp / log errors (r3dg_expf <= 0.9 ulp, __logf). The term
+// e * Mmax absorbs the fp32 rounding of Q itself: the blend's gauss_power rounds ~7 times and the
+// cull's own minimum ~5 times, each error bounded by 2^-24 times the term magnitudes
+// |a| dx^2 + 2 |b dx dy| + |c| dy^2 <= (|a| + |b|) dx^2 + (|c| + |b|) dy^2, whose maximum over the
+// quadrant rectangle is Mmax. For compact splats Mmax is small and the term vanishes; for large,
+// needle-shaped splats far from their mean the terms reach ~1e6 and cancel to a few units, and the
+// term keeps the cull conservative there (tests/test_gpu_parity.py test_cull_exact_needles:
+// cull on == off bit for bit on 1920x1080 needles with sigma up to 1000 px). Round 1 used m = 0.1.
 #ifndef R3DG_CULL_MARGIN
 #define R3DG_CULL_MARGIN 0.01f
 #endif
+#ifndef R3DG_CULL_REL
+#define R3DG_CULL_REL 1e-6f  // e: 16 * 2^-24 rounded up
+#endif
+
+// Is min Q over the pixel rectangle [xa, xb] x [ya, yb] above t (1 + m) + m + e * Mmax, i.e. does
+// alpha = o exp(-Q/2) stay below 1/255 at every pixel of the rectangle, in the blend's own fp32
+// arithmetic? (a, b, c) = conic, (mx, my) = mean, lt = 2 ln(255 o).
+__device__ __forceinline__ bool rect_culled(float4 co, float mx, float my, float xa, float xb, float ya,
+                                            float yb) {
+    const float ia = __builtin_amdgcn_rcpf(co.x), ic = __builtin_amdgcn_rcpf(co.z);
+    const float qmin = qform_min_rect(co.x, co.y, co.z, ia, ic, mx, my, xa, xb, ya, yb);
+    const float dxa = mx - xa, dxb = mx - xb, dya = my - ya, dyb = my - yb;
+    const float ab = fabsf(co.y);
+    const float mmax = (co.x + ab) * fmaxf(dxa * dxa, dxb * dxb) + (co.z + ab) * fmaxf(dya * dya, dyb * dyb);
+    const float t = 2.0f * __logf(255.0f * co.w) * (1.0f + R3DG_CULL_MARGIN) + R3DG_CULL_MARGIN +
+                    R3DG_CULL_REL * mmax;
+    return qmin > t;  // false for a NaN / infinite bound: keep
+}
 
 // quadrant_mask's test for one quadrant with top-left pixel (qx, qy): may alpha reach 1/255 there
 // (bit q of quadrant_mask(xy, co, x0, y0, cull) for qx = x0 + (q & 1) * 8, qy = y0 + (q >> 1) * 8).
@@ -296,32 +319,22 @@ __device__ __forceinline__ bool quadrant_live(float2 xy, float4 co, float qx, fl
     if (co.w < 1.0f / 255.0f) return false;
     const float det = co.x * co.z - co.y * co.y;
     if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return true;
-    const float t = 2.0f * __logf(255.0f * co.w) * (1.0f + R3DG_CULL_MARGIN) + R3DG_CULL_MARGIN;
-    if (!(t < 1e30f)) return true;
-    const float ia = __builtin_amdgcn_rcpf(co.x), ic = __builtin_amdgcn_rcpf(co.z);
-    return !(qform_min_rect(co.x, co.y, co.z, ia, ic, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f) > t);
+    return !rect_culled(co, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f);
 }
 
 // Conservative set of the 8x8 quadrants of tile (x0, y0) in which alpha = o exp(-Q/2) can reach
-// 1/255, i.e. Q <= 2 ln(255 o). A quadrant is dropped only if the minimum of Q over its pixel
-// rectangle exceeds t = 2 ln(255 o) (1 + m) + m (R3DG_CULL_MARGIN), so a dropped instance fails
-// the reference's alpha test on every pixel of the quadrant (tests/test_gpu_parity.py: cull on ==
-// off bitwise).
+// 1/255 (rect_culled's margin), so a dropped instance fails the reference's alpha test on every
+// pixel of the quadrant (tests/test_gpu_parity.py: cull on == off bitwise).
 __device__ __forceinline__ uint32_t quadrant_mask(float2 xy, float4 co, int x0, int y0, int cull) {
     if (!cull) return 0xFu;
     if (co.w < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 everywhere
     const float det = co.x * co.z - co.y * co.y;
     if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return 0xFu;
-    const float t = 2.0f * __logf(255.0f * co.w) * (1.0f + R3DG_CULL_MARGIN) + R3DG_CULL_MARGIN;
-    if (!(t < 1e30f)) return 0xFu;
-    // approximate reciprocals: an inexact minimiser changes Q only at second order
-    const float ia = __builtin_amdgcn_rcpf(co.x), ic = __builtin_amdgcn_rcpf(co.z);
     uint32_t m = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const float qx = (float)(x0 + (q & 1) * 8), qy = (float)(y0 + (q >> 1) * 8);
-        const float qmin = qform_min_rect(co.x, co.y, co.z, ia, ic, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f);
-        if (!(qmin > t)) m |= 1u << q;
+        if (!rect_culled(co, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f)) m |= 1u << q;
     }
     return m;
 }

@@ -57,6 +57,7 @@ struct RenderFwdArgs {
     float* out_feature;
     float* out_shader_color;
     float* zero_stencil;  // stencil output to zero (default splat shaders), or null
+    uint8_t* contrib;     // [L] per sorted position: bit q set when a pixel of quadrant q blended it
     FeatureLayout flay;
 };
 
@@ -97,7 +98,8 @@ struct RenderBwdArgs {
     int S, W, H, grid_x, grid_y, num_tiles, cull, backward_geometry, RS;
     const uint32_t* tile_order;  // launch order of the tiles (longest first), or null
     float* rows;               // [4L, RS] partial rows (part_row_stride)
-    uint8_t* flags;            // [4L] 1 where a partial row was written (zeroed by the host)
+    uint8_t* flags;            // [4L] 1 where a partial row was written (zeroed by the forward's duplicate pass)
+    const uint8_t* contrib;    // [L] the forward's contribution bits (RenderFwdArgs::contrib)
 };
 
 struct GatherBwdArgs {

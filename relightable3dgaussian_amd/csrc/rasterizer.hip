@@ -118,6 +118,7 @@ static BinningState carve_binning(uintptr_t p, size_t L, uintptr_t* end) {
     b.point_list = carve<uint32_t>(p, L);
     b.keys2 = carve<uint32_t>(p, L);
     b.flags = carve<uint32_t>(p, L);
+    b.contrib = carve<uint8_t>(p, L);
     b.sort_temp_bytes = sort_temp_size(L);
     b.sort_temp = carve<char>(p, b.sort_temp_bytes);
     if (end) *end = p;
@@ -201,6 +202,7 @@ struct ProfScope {
 struct Readback {
     uint32_t* host = nullptr;
     hipEvent_t ev = nullptr;
+    uint32_t* dev_flag = nullptr;  // preprocess error flag (prefiltered runs only)
 };
 static hipError_t readback_slot(Readback** out) {
     constexpr int kMaxDevices = 64;
@@ -374,6 +376,7 @@ extern "C" int r3dg_feature_groups(int S, int* groups) {
 }
 
 extern "C" size_t r3dg_image_state_n_contrib_offset(int H, int W) { return align256(4 * (size_t)H * W); }
+extern "C" size_t r3dg_geom_state_bytes(int P, int S) { return geom_state_bytes(P > 0 ? (size_t)P : 0, S); }
 
 extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3dg_gaussians* g,
                                         const r3dg_forward_outputs* out, r3dg_alloc_fn geom_alloc, void* geom_ctx,
@@ -554,6 +557,16 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         pa.depths = geom.depths;
         pa.means2D = geom.means2D; pa.cov3D = geom.cov3D; pa.conic_opacity = geom.conic_opacity;
         pa.rgb = geom.rgb; pa.clamped = geom.clamped; pa.error_flag = nullptr;
+        Readback* rb = nullptr;
+        R3DG_CHECK_HIP(readback_slot(&rb));
+        if (s->prefiltered) {
+            // the reference __trap()s on a point the frustum test drops although the caller
+            // promised a prefiltered set (auxiliary.h:154-160); here the kernel raises a flag and
+            // the call fails with R3DG_ERR_ARG
+            if (!rb->dev_flag) R3DG_CHECK_HIP(hipMalloc(&rb->dev_flag, sizeof(uint32_t)));
+            R3DG_CHECK_HIP(hipMemsetAsync(rb->dev_flag, 0, sizeof(uint32_t), st));
+            pa.error_flag = rb->dev_flag;
+        }
         {
             ProfScope ps(R3DG_PROF_PREPROCESS, st);
             launch_kernel(preprocess_kernel, dim3((P + 255) / 256), dim3(256), st, pa);
@@ -565,13 +578,16 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
                                                (size_t)P, rocprim::plus<uint32_t>(), st));
         // num_rendered (rasterizer_impl.cu:259-263 reads it with a blocking cudaMemcpy): one 4-byte
         // copy into pinned host memory and a wait on an event behind that copy only
-        Readback* rb = nullptr;
-        R3DG_CHECK_HIP(readback_slot(&rb));
         R3DG_CHECK_HIP(hipMemcpyAsync(rb->host, geom.point_offsets + P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                       st));
+        if (s->prefiltered)
+            R3DG_CHECK_HIP(hipMemcpyAsync(rb->host + 1, rb->dev_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         R3DG_CHECK_HIP(hipEventRecord(rb->ev, st));
         R3DG_CHECK_HIP(hipEventSynchronize(rb->ev));
         const uint32_t Lh = *rb->host;
+        R3DG_REQUIRE(!s->prefiltered || rb->host[1] == 0,
+                     "rasterize_gaussians: point is filtered although prefiltered is set (the reference traps, "
+                     "auxiliary.h:156-160)");
         R3DG_REQUIRE(Lh < (1u << 31), "rasterize_gaussians: too many tile instances");
         L = (int)Lh;
     }
@@ -671,6 +687,7 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     // default splat shaders leave every stencil value 0 (InitializeStencil, rasterizer_impl.cu:203-209):
     // the blend writes those zeros with its other outputs (no separate memset launch)
     ra.zero_stencil = splat_active ? nullptr : out->stencil;
+    ra.contrib = bin.contrib;
     if (const char* e = getenv("R3DG_NO_CULL")) ra.cull = (e[0] == '0');
     {
         ProfScope ps(R3DG_PROF_RENDER_FWD, st);
@@ -751,8 +768,8 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     // scratch: partial rows [4L, RS] (one per instance and quadrant, written sparsely) and the
     // per-Gaussian sums [P, RS]; the rows' presence flags live in the binning state, zeroed by the
     // forward's duplicate pass (a row's presence depends on the forward state only)
-    // the backward blend addresses partial rows with 32-bit element offsets
-    R3DG_REQUIRE((size_t)RS * 4 * (size_t)L < (1ull << 31), "rasterize_gaussians_backward: too many tile instances");
+    // the backward blend addresses partial rows with 32-bit offsets in float4 units
+    R3DG_REQUIRE((size_t)RS * (size_t)L < (1ull << 32), "rasterize_gaussians_backward: too many tile instances");
     const size_t row_bytes = sizeof(float) * (size_t)RS * 4 * L;
     const size_t sum_bytes = sizeof(float) * (size_t)RS * P;
     char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + sum_bytes);
@@ -795,6 +812,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         ba.RS = RS;
         ba.rows = rows;
         ba.flags = flags;
+        ba.contrib = bs.contrib;
         {
             ProfScope ps(R3DG_PROF_RENDER_BWD, st);
             R3DG_CHECK_HIP(launch_render_backward(ba, st));

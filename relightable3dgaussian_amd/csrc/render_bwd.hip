@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
             s_xy[t] = make_float2(r1.x, r1.y);
             s_co[t] = co;
             s_slot[t] = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
-            s_mask[t] = quadrant_mask(make_float2(r1.x, r1.y), co, tx * kTileX, ty * kTileY, a.cull);
+            s_mask[t] = a.contrib[range.x + (uint32_t)(hi - 1 - t)];  // the forward's contribution bits
 #pragma unroll
             for (int q = 0; q < NA4; ++q) s_attr[t * NA4 + q] = rec[2 + q];
         }
@@ -225,12 +225,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // Tuning knobs (experiment builds override them through R3DG_EXTRA_HIPFLAGS). Occupancy is set
 // by LDS and VGPRs together; the LDS allocation is rounded up in 2 KiB steps.
-#ifndef R3DG_BWD_NB
-#define R3DG_BWD_NB 64  // instances staged per batch
-#endif
-#ifndef R3DG_BWD_PKDOT
-#define R3DG_BWD_PKDOT 1  // the per-pixel channel dot as packed fp32 FMAs
-#endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 #ifndef R3DG_BWD_WAVES
 #define R3DG_BWD_WAVES 4  // waves per SIMD the register allocation targets (SMAX <= 12)
@@ -249,9 +243,6 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
-#ifndef R3DG_BWD_SKIP_EMPTY
-#define R3DG_BWD_SKIP_EMPTY 1  // DMA-staged kernel: instances no pixel of the wave blended get no row
-#endif
 #ifndef R3DG_BWDG_NB
 #define R3DG_BWDG_NB 64  // instances per staged batch of the DMA-staged kernel
 #endif
@@ -259,339 +250,23 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
 #define R3DG_BWDG_GRP 13  // instances per MFMA group of the DMA-staged kernel (64 / 13 measured best of
                           // 32 / 16, 64 / 12, 64 / 13, 32 / 12: the smaller w|q image buys the larger batch)
 #endif
-#ifndef R3DG_BWDG_PWNB
-#define R3DG_BWDG_PWNB 16  // instances per staged batch of the per-wave DMA variant
-#endif
-#ifndef R3DG_BWDW_NB
-#define R3DG_BWDW_NB 32  // instances staged per batch by a one-wave workgroup
-#endif
-
-// PW = false: one 256-thread workgroup per tile, wave w = quadrant w, staging shared by the four
-// waves (two block barriers per batch). PW = true: one 64-thread workgroup per (tile, quadrant),
-// staging private to the wave, no block barriers -- a wave never waits for the other quadrants of
-// its tile (their live-instance counts and n_contrib depths differ widely) and iterates only up to
-// its own n_contrib maximum. The four quadrant workgroups of a tile are blocks b, b+8, b+16, b+24,
-// so they share an XCD (and its L2 copy of the tile's render records).
-template <int SMAX, bool PW>
-__global__ void __launch_bounds__(PW ? 64 : kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
-render_bwd_mfma_kernel(RenderBwdArgs a) {
-    constexpr int NB = PW ? R3DG_BWDW_NB : R3DG_BWD_NB;
-    constexpr int NW = PW ? 1 : 4;                // waves per workgroup
-    constexpr int NA4 = (4 + SMAX + 3) / 4;       // staged attribute row: colour, depth, features
-    constexpr int NXB = (4 + SMAX + 15) / 16;     // 16-channel blocks of X = [g0..2, gf0..S-1, gd]
-    constexpr int XW = 16 * NXB;
-    constexpr int GRP = 16;                       // instances per MFMA group
-    constexpr int RF4 = 2 + NA4;                  // float4s per render record in HBM
-    constexpr int SF4 = 1 + NA4;                  // staged: conic|opacity, attribute row
-    __shared__ float4 s_rec[NB * SF4];            // one base address per instance
-    __shared__ float2 s_xy[NB];
-    __shared__ uint32_t s_slot[NB];
-    __shared__ uint32_t s_bits[PW ? 1 : NB / 32][4];  // [chunk][wave] live-instance masks (PW: unused)
-    __shared__ float s_wq[NW][2 * GRP * WQS];     // per wave: w rows 0..15, q rows 16..31
-    __shared__ int s_max_last;
-
-    int tile, w;
-    if constexpr (PW) {
-        const int b = blockIdx.x, xcd = b & 7, k = b >> 3;
-        w = k & 3;
-        const int vb = ((k >> 2) << 3) | xcd;  // this tile's position in the tile launch order
-        tile = a.tile_order ? (vb < a.num_tiles ? (int)a.tile_order[vb] : a.num_tiles)
-                            : xcd_tile(vb, (int)gridDim.x >> 2);
-    } else {
-        tile = block_tile(a.tile_order, a.num_tiles);
-        w = threadIdx.x >> 6;
-    }
-    if (tile >= a.num_tiles) return;
-    const int t = threadIdx.x, l = t & 63;
-    R3DG_BWD_PIXELS()
-    float T = T_final;
-
-    // ---- B operands: X[pixel][channel] and Y[pixel][moment] for k-step s (pixel 4s + (l>>4)) ----
-    float* wq = s_wq[PW ? 0 : w];
-    float bX[NXB][16];
-    // Y[pixel][moment] = [1, x, y, x^2, xy, y^2][nch] at pixel 4*s2 + (l>>4) of this wave, offsets
-    // from the quadrant centre: x depends only on s2&1 and y = (s2>>1) - 3.5 is wave-uniform per
-    // s2, so the B operand of k-step s2 is yA[s2&1] + y*(yB[s2&1] + y*yC) (exact: every term but
-    // one is a zero product).
-    {
-#pragma unroll
-        for (int xb = 0; xb < NXB; ++xb) {
-#pragma unroll
-            for (int c = 0; c < 16; ++c) {
-                const int ch = xb * 16 + c;
-                float v = 0.f;
-                if (ch < 3) v = g[ch];
-                else if (ch - 3 < SMAX && ch - 3 < S) v = gf[(ch - 3) < SMAX ? (ch - 3) : 0];
-                else if (ch == 3 + S) v = gd;
-                wq[c * WQS + l] = v;
-            }
-            wave_lds_sync();
-#pragma unroll
-            for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
-            wave_lds_sync();
-        }
-    }
-
-    // The reference keeps one accum_rec per channel (colour, features, depth) and accum_opa; all
-    // share the same alpha recurrence and enter dL/dalpha only through their dot with the upstream
-    // gradient, so one scalar u = sum_c accum_rec[c] * dL_dchannel[c] + dL_dopacity * accum_opa
-    // carries them all. With d = colour.g + dL_dopacity: dL/dalpha = (d - u) * T' - T_final /
-    // (1 - alpha) * bg.g, then u += alpha * (d - u) -- the reference's delayed last_alpha /
-    // last_color update applied at the end of each contributing step instead. A non-contributing
-    // step runs with alpha = 0, which leaves T (1/(1-0) = 1 exactly) and u unchanged.
-    if (!a.backward_geometry) {
-#pragma unroll
-        for (int c = 0; c < SMAX; ++c) gf[c] = 0.f;  // bX already holds the feature grads
-    }
-    // upstream gradients in the staged attribute order [r, g, b, depth, f0 ..] as packed pairs
-    f32x2 gp[2 * NA4];
-#pragma unroll
-    for (int c2 = 0; c2 < 2 * NA4; ++c2) {
-        float e[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int ch = 2 * c2 + h;
-            e[h] = ch < 3 ? g[ch] : (ch == 3 ? gd : (ch - 4 < SMAX ? gf[(ch - 4) < SMAX ? ch - 4 : 0] : 0.f));
-        }
-        gp[c2] = f32x2{e[0], e[1]};
-    }
-    float u = 0.f;
-    const float TFB = T_final * bg_dot;
-    int rowj = 0;  // lane k: partial-row index (4 * slot + wave) of MFMA group row k
-
-    const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
-    const int max_last = PW ? wmax : block_max_last(wmax, &s_max_last);
-    const int RS = a.RS;
-    const int nch = l & 15;
-
-    // One blend step of the reference's per-pixel loop (backward.cu:520-611), predicated rather
-    // than branched: every LDS read is issued up front and a non-contributing pixel (outside,
-    // past n_contrib, power > 0 or alpha < 1/255) leaves its state unchanged.
-    // `power` (the forward's bits) and G (fast exp, alpha test settled exactly) come from the caller.
-    auto step = [&](int j, int p, bool live, float opacity, float power, float G, float& wv, float& qv) {
-#pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
-        const int ju = __builtin_amdgcn_readfirstlane(j);  // uniform addresses
-        const float4* rj = s_rec + ju * SF4;
-        float v[NA4 * 4];
-#pragma unroll
-        for (int q = 0; q < NA4; ++q) {
-            const float4 rr = rj[1 + q];
-            v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
-        }
-        const float alpha = fminf(0.99f, opacity * G);
-        // p < last is false for pixels outside the image (last = 0 there)
-        const bool ok = live && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-        const float ae = ok ? alpha : 0.f;
-        const float Ge = ok ? G : 0.f;
-        const float rinv = __builtin_amdgcn_rcpf(1.f - ae);
-        const float Tn = T * rinv;
-#ifdef R3DG_EXP_NODOT  // timing experiment only: drop the per-pixel colour/feature dot
-        float d = go + v[0];
-#elif R3DG_BWD_PKDOT
-        // packed: v_pk_fma_f32 over (channel 2c, 2c+1) pairs, two partial sums
-        f32x2 d2 = {go, 0.f};
-#pragma unroll
-        for (int c2 = 0; c2 < 2 * NA4; ++c2)
-            d2 = __builtin_elementwise_fma(f32x2{v[2 * c2], v[2 * c2 + 1]}, gp[c2], d2);
-        float d = d2.x + d2.y;
-#else
-        float d = __builtin_fmaf(v[0], g[0], go);
-        d = __builtin_fmaf(v[1], g[1], d);
-        d = __builtin_fmaf(v[2], g[2], d);
-        d = __builtin_fmaf(v[3], gd, d);
-#pragma unroll
-        for (int c2 = 0; c2 < SMAX; ++c2) d = __builtin_fmaf(v[4 + c2], gf[c2], d);
-#endif
-        const float diff = d - u;
-        const float dL_dalpha = rinv * __builtin_fmaf(T, diff, -TFB);
-        wv = ae * Tn;
-        qv = Ge * dL_dalpha;
-        T = Tn;
-        u = __builtin_fmaf(ae, diff, u);
-    };
-
-    // [16 w rows] x X and [16 q rows] x Y over the wave's 64 pixels; rows >= r hold stale values
-    // whose results are discarded (an output row depends on its A row only).
-    auto flush = [&](int r) {
-        if (l == 0) R3DG_EXP_ADD(1, 1);
-#ifdef R3DG_EXP_NOFLUSH  // timing experiment only: no flush products
-        return;
-#endif
-        // the Y operand coefficients, rebuilt per flush from the lane id (5 fewer live VGPRs in
-        // the step loop)
-        float yA[2], yB[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const float xo = (float)(4 * h + (l >> 4)) - 3.5f;
-            yA[h] = nch == 0 ? 1.f : (nch == 1 ? xo : (nch == 3 ? xo * xo : 0.f));
-            yB[h] = nch == 2 ? 1.f : (nch == 4 ? xo : 0.f);
-        }
-        const float yC = nch == 5 ? 1.f : 0.f;
-        wave_lds_sync();
-        floatx4 accX[NXB], accY = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int xb = 0; xb < NXB; ++xb) accX[xb] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) {
-            const int col = 4 * s2 + (l >> 4);
-            const float av = wq[(l & 15) * WQS + col];
-            const float aq = wq[(GRP + (l & 15)) * WQS + col];
-#ifdef R3DG_EXP_NOMFMA  // timing experiment only: A reads and stores without the products
-            accX[0][0] += av;
-            accY[0] += aq;
-#else
-#pragma unroll
-            for (int xb = 0; xb < NXB; ++xb)
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
-            const float yo = (float)(s2 >> 1) - 3.5f;
-            const float by = yA[s2 & 1] + yo * (yB[s2 & 1] + yo * yC);
-            accY = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, by, accY, 0, 0, 0);
-#endif
-        }
-        // D row 4*(l>>4)+i (group instance), column l&15 (channel / moment) -> partial row
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = (l >> 4) * 4 + i;
-            const uint32_t base = (uint32_t)__shfl(rowj, row);  // partial row of group row `row`
-#ifdef R3DG_EXP_NOSTORE  // timing experiment only: products without the row stores
-            if (row < r && a.S < 0) {
-#else
-            if (row < r) {
-#endif
-                float* dst = a.rows + (size_t)base * RS;
-#pragma unroll
-                for (int xb = 0; xb < NXB; ++xb) dst[xb * 16 + nch] = accX[xb][i];
-                if (nch < 6) dst[XW + nch] = accY[i];
-                if (nch == 0) a.flags[base] = 1;
-            }
-        }
-        wave_lds_sync();
-    };
-
-    int r = 0;  // rows filled in the current MFMA group
-#ifdef R3DG_EXP_COUNT
-    const long long t_begin = wall_clock64();
-    long long t_stage = 0;
-#endif
-    // Gaussian ids of the next batch, loaded one batch ahead: staging then waits for one
-    // dependent memory round trip (the render records) instead of two
-    uint32_t gid_next = t < min(NB, max_last) ? a.point_list[range.x + (uint32_t)(max_last - 1 - t)] : 0u;
-    for (int hi = max_last; hi > 0; hi -= NB) {
-        const int cnt = min(NB, hi);
-#ifdef R3DG_EXP_COUNT
-        const long long ts0 = wall_clock64();
-#endif
-        if constexpr (PW) wave_lds_sync();  // this wave's reads of the previous batch are done
-        else __syncthreads();
-        uint32_t m = 0;
-        if (t < cnt) {
-            const uint32_t gid = gid_next;
-            // one contiguous render record per Gaussian (r3dg_kernels.h record_f4), staged verbatim
-            const float4* rec = a.records + (size_t)gid * RF4;
-            float4 rv[RF4];
-#pragma unroll
-            for (int q = 0; q < RF4; ++q) rv[q] = rec[q];
-            const int hn = hi - NB;
-            gid_next = (hn > 0 && t < min(NB, hn)) ? a.point_list[range.x + (uint32_t)(hn - 1 - t)] : 0u;
-            s_rec[t * SF4] = rv[0];
-#pragma unroll
-            for (int q = 0; q < NA4; ++q) s_rec[t * SF4 + 1 + q] = rv[2 + q];
-            s_xy[t] = make_float2(rv[1].x, rv[1].y);
-            s_slot[t] = record_slot(rv[1], tx, ty, a.grid_x, a.grid_y);
-            m = quadrant_mask(make_float2(rv[1].x, rv[1].y), rv[0], tx * kTileX, ty * kTileY, a.cull);
-        }
-        unsigned long long live = 0;  // PW: this quadrant's live instances of the batch
-        if constexpr (PW) {
-            live = __ballot((m >> w) & 1u);
-            wave_lds_sync();
-        } else {
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const unsigned long long bal = __ballot((m >> b) & 1u);
-                if (l == 0 && w < NB / 64) {
-                    s_bits[2 * w][b] = (uint32_t)bal;
-                    s_bits[2 * w + 1][b] = (uint32_t)(bal >> 32);
-                }
-            }
-            __syncthreads();
-        }
-#ifdef R3DG_EXP_COUNT
-        t_stage += wall_clock64() - ts0;
-#endif
-        const int jmin = hi - wmax;  // instances j < jmin lie beyond every pixel of this wave
-        for (int c = 0; c * 32 < cnt; ++c) {
-            uint32_t bits = PW ? (uint32_t)(live >> (32 * c)) : __builtin_amdgcn_readfirstlane(s_bits[c][w]);
-            const int lo = jmin - c * 32;
-            if (lo >= 32) bits = 0;
-            else if (lo > 0) bits &= ~0u << lo;
-            if (l == 0) R3DG_EXP_ADD(0, __builtin_popcount(bits));
-            // two compacted instances per iteration: the second one's LDS reads and exp overlap
-            // the first one's dependent chain
-            auto take = [&](int& ja, int& jb, bool& hb) {
-                ja = c * 32 + __builtin_ctz(bits);
-                bits &= bits - 1;
-                hb = bits != 0u;
-                jb = hb ? c * 32 + __builtin_ctz(bits) : ja;
-                bits &= bits - 1;
-            };
-            auto rec0 = [&](int j) { return s_rec[__builtin_amdgcn_readfirstlane(j) * SF4]; };
-            auto pos = [&](int j) { return s_xy[__builtin_amdgcn_readfirstlane(j)]; };
-            while (bits) {
-                int j0, j1;
-                bool has1;
-                take(j0, j1, has1);
-                const float4 co0 = rec0(j0), co1 = rec0(j1);
-                const float2 xy0 = pos(j0), xy1 = pos(j1);
-                const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);  // the forward's bits
-                const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
-                float G0 = fast_expf(pw0), G1 = fast_expf(pw1);
-                settle_threshold2(pw0, co0.w, G0, pw1, co1.w, G1);
-                float wv0, qv0, wv1, qv1;
-                step(j0, hi - 1 - j0, true, co0.w, pw0, G0, wv0, qv0);
-                step(j1, hi - 1 - j1, has1, co1.w, pw1, G1, wv1, qv1);
-                float* wr = wq + r * WQS + l;
-                wr[0] = wv0;
-                wr[GRP * WQS] = qv0;
-                wr[WQS] = wv1;
-                wr[(GRP + 1) * WQS] = qv1;
-                // group row -> partial row (4 * slot + wave), kept in lane `row` of rowj: the
-                // group does not depend on the staging arrays and fills across batches
-                rowj = write_lane(rowj, (int)(s_slot[j0] * 4 + w), r);
-                rowj = write_lane(rowj, (int)(s_slot[j1] * 4 + w), r + 1);
-                r += has1 ? 2 : 1;
-                if (r > GRP - 2) {
-                    flush(r);
-                    r = 0;
-                }
-            }
-        }
-    }
-    if (r > 0) flush(r);
-#ifdef R3DG_EXP_COUNT
-    if (l == 0) {
-        R3DG_EXP_ADD(2, t_stage);                   // staging + its two barriers, per wave
-        R3DG_EXP_ADD(3, wall_clock64() - t_begin);  // batch loop total, per wave
-    }
-#endif
-}
 
 // ---------------------------------------------------------------------------------------------
-// Double-buffered variant: the render records of batch b+1 are copied HBM -> LDS by LDS-DMA
+// The backward blend (default). One 256-thread workgroup per tile (longest tiles first), wave w =
+// quadrant w. The render records of batch b+1 are copied HBM -> LDS by LDS-DMA
 // (global_load_lds_dwordx4, no VGPRs) while the waves blend batch b, so the record round trip is
-// off the critical path and a batch costs one block barrier instead of two. Every wave evaluates
-// the quadrant cull of the staged instances for its own quadrant (ballot -> live mask in SGPRs)
-// and reads an instance's slot from the lane that computed it, so nothing but the records goes
-// through LDS. Staging buffer layout: column q (float4 q of the record) of instance t at
-// [q * NB + t], two columns per DMA wave-instruction (lanes 0-31 column 2k, lanes 32-63 column
-// 2k+1). Same blend step, MFMA flush and partial rows as render_bwd_mfma_kernel.
+// off the critical path and a batch costs one block barrier. A wave visits exactly the staged
+// instances that at least one of its pixels blended in the forward: the forward's contribution
+// bits (render_fwd.hip, one byte per sorted position, bit = quadrant), loaded one batch ahead --
+// no footprint cull here and no instance without a partial row. The instance's slot comes from
+// the lane that loaded its bits (record_slot), so nothing but the records goes through LDS.
+// Staging buffer layout: column q (float4 q of the record) of instance t at [q * NB + t].
 // ---------------------------------------------------------------------------------------------
-// PW = true: one 64-thread workgroup per (tile, quadrant) with its own (smaller) staging double
-// buffer: no block barriers, and a wave stages only up to its own n_contrib maximum.
-template <int SMAX, bool PW>
-__global__ void __launch_bounds__(PW ? 64 : kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
+template <int SMAX>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
 render_bwd_glds_kernel(RenderBwdArgs a) {
-    constexpr int NB = PW ? R3DG_BWDG_PWNB : R3DG_BWDG_NB;  // instances per batch (two batches staged)
-    constexpr int NW = PW ? 1 : 4;                // waves per workgroup
+    constexpr int NB = R3DG_BWDG_NB;              // instances per batch (two batches staged)
+    constexpr int NW = 4;                         // waves per workgroup
     constexpr int NA4 = (4 + SMAX + 3) / 4;
     constexpr int NXB = (4 + SMAX + 15) / 16;
     constexpr int XW = 16 * NXB;
@@ -611,23 +286,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     __shared__ float4 s_lds[NW * WQF4 + 2 * SBUF + 1];
     float4* const stage = s_lds + NW * WQF4;
 
-    int tile, w;
-    if constexpr (PW) {
-        // the four quadrant workgroups of a tile are blocks b, b+8, b+16, b+24: one XCD
-        const int b = blockIdx.x, xcd = b & 7, k = b >> 3;
-        w = k & 3;
-        const int vb = ((k >> 2) << 3) | xcd;
-        tile = a.tile_order ? (vb < a.num_tiles ? (int)a.tile_order[vb] : a.num_tiles)
-                            : xcd_tile(vb, (int)gridDim.x >> 2);
-    } else {
-        tile = block_tile(a.tile_order, a.num_tiles);
-        w = threadIdx.x >> 6;
-    }
+    const int tile = block_tile(a.tile_order, a.num_tiles);
+    const int w = threadIdx.x >> 6;
     if (tile >= a.num_tiles) return;
     const int t = threadIdx.x, l = t & 63;
     R3DG_BWD_PIXELS()
     float T = T_final;
-    float* wq = reinterpret_cast<float*>(s_lds + (PW ? 0 : w) * WQF4);
+    float* wq = reinterpret_cast<float*>(s_lds + w * WQF4);
     int* s_max_last = reinterpret_cast<int*>(stage + 2 * SBUF);
 
     float bX[NXB][16];
@@ -668,11 +333,10 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     const float TFB = T_final * bg_dot;
     int rowj = 0;
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
-    const int max_last = PW ? wmax : block_max_last(wmax, s_max_last);
+    const int max_last = block_max_last(wmax, s_max_last);
     const int RS = a.RS;
     const int nch = l & 15;
     const float4* st = stage;  // staging buffer of the current batch
-    const float qx0 = (float)(tx * kTileX + (w & 1) * 8), qy0 = (float)(ty * kTileY + (w >> 1) * 8);
 
     auto step = [&](int j, int p, bool live, float opacity, float power, float G, float& wv, float& qv,
                     bool& okv) {
@@ -735,8 +399,9 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             const int row = (l >> 4) * 4 + i;
             const uint32_t base = (uint32_t)__shfl(rowj, row);
             if (row < r) {
-                // 32-bit element offset: 4L rows x RS floats stay below 2^31 (checked on the host)
-                float* dst = a.rows + (uint32_t)(base * (uint32_t)RS);
+                // 32-bit offset in float4 units (RS is a multiple of 8 floats): 4L rows x RS / 4
+                // stay below 2^32 (checked on the host: L * RS < 2^32, L < 178M at S <= 12)
+                float* dst = reinterpret_cast<float*>(reinterpret_cast<float4*>(a.rows) + base * (uint32_t)(RS >> 2));
 #pragma unroll
                 for (int xb = 0; xb < NXB; ++xb) dst[xb * 16 + nch] = accX[xb][i];
                 if (nch < 6) dst[XW + nch] = accY[i];
@@ -759,7 +424,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     auto issue = [&](uint32_t gid, int buf) {
 #pragma unroll
         for (int k = 0; k < NCP; ++k) {
-            if (!PW && (k & 3) != w) continue;  // wave-uniform
+            if ((k & 3) != w) continue;  // wave-uniform
             // lane l of instruction k: entry k * 64 + l = column q, instance l % NB
             const int q = (k * 64 + l) / NB;
             const float4* src = a.records + (size_t)gid * RF4 + min(q, RF4 - 1);
@@ -773,12 +438,16 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         }
     };
 
+    // contribution byte of instance l of the batch ending at tile position hi_b (0 past the batch)
+    auto batch_bits = [&](int hi_b) -> uint32_t {
+        return l < min(NB, hi_b) ? (uint32_t)a.contrib[range.x + (uint32_t)(hi_b - 1 - l)] : 0u;
+    };
     int r = 0;
     if (max_last > 0) issue(batch_gid(max_last), 0);
     uint32_t gid_next = max_last > NB ? batch_gid(max_last - NB) : 0u;
+    uint32_t cb_next = max_last > 0 ? batch_bits(max_last) : 0u;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (PW) wave_lds_sync();
-    else __syncthreads();
+    __syncthreads();
     int buf = 0;
 #ifdef R3DG_EXP_COUNT
     const long long t_begin = wall_clock64();
@@ -790,19 +459,18 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #ifdef R3DG_EXP_COUNT
         const long long tm0 = wall_clock64();
 #endif
+        const uint32_t cbits = cb_next;
         if (hn > 0) {  // block-uniform: stage the next batch while this one blends
             issue(gid_next, buf ^ 1);
             gid_next = hn > NB ? batch_gid(hn - NB) : 0u;
+            cb_next = batch_bits(hn);
         }
         st = stage + buf * SBUF;
-        // this wave's live instances: the cull for its own quadrant, evaluated by lanes 0..cnt-1
+        // this wave's live instances: the forward's contribution bits for its quadrant (lanes
+        // 0..cnt-1; zero past the batch)
         uint32_t slot_l = 0u;
-        bool mine = false;
-        if (l < cnt) {
-            const float4 co = st[l], r1 = st[NB + l];
-            slot_l = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
-            mine = quadrant_live(make_float2(r1.x, r1.y), co, qx0, qy0, a.cull);
-        }
+        const bool mine = (cbits >> w) & 1u;
+        if (mine) slot_l = record_slot(st[NB + l], tx, ty, a.grid_x, a.grid_y);
         mask_t bits = (mask_t)__ballot(mine);
         const int lo = hi - wmax;  // instances j < lo lie beyond every pixel of this wave
         if (lo >= NB) bits = 0u;
@@ -831,28 +499,32 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             bool ok0, ok1;
             step(j0, hi - 1 - j0, true, co0.w, pw0, G0, wv0, qv0, ok0);
             step(j1, hi - 1 - j1, has1, co1.w, pw1, G1, wv1, qv1, ok1);
-            // an instance no pixel of this wave blended (the cull is conservative; pixels may sit
-            // past their n_contrib) has w = q = 0 on every lane: it joins no MFMA group and gets no
-            // partial row (its flag stays 0; the row-sum adds nothing for it either way)
-#if R3DG_BWD_SKIP_EMPTY
-            const bool any0 = __ballot(ok0) != 0ull, any1 = __ballot(ok1) != 0ull;
+#ifdef R3DG_EXP_COUNT
+            {
+                const unsigned long long b0 = __ballot(ok0), b1 = __ballot(ok1);
+                if (l == 0) {
+                    R3DG_EXP_ADD(5, (b0 != 0ull ? 1 : 0) + (b1 != 0ull ? 1 : 0));
+                    R3DG_EXP_ADD(6, __builtin_popcountll(b0) + __builtin_popcountll(b1));
+                }
+            }
 #else
-            const bool any0 = true, any1 = has1;
+            (void)ok0;
+            (void)ok1;
 #endif
-            if (any0) {
+            // every visited instance was blended by a pixel of this wave: one group row each
+            {
                 float* wr = wq + r * WQS + l;
                 wr[0] = wv0;
                 wr[GRP * WQS] = qv0;
                 rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j0) * 4 + w), r);
             }
-            const int r1 = r + (any0 ? 1 : 0);
-            if (any1) {
-                float* wr = wq + r1 * WQS + l;
+            if (has1) {
+                float* wr = wq + (r + 1) * WQS + l;
                 wr[0] = wv1;
                 wr[GRP * WQS] = qv1;
-                rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j1) * 4 + w), r1);
+                rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j1) * 4 + w), r + 1);
             }
-            r = r1 + (any1 ? 1 : 0);
+            r += has1 ? 2 : 1;
             if (r > GRP - 2) {
                 flush(r);
                 r = 0;
@@ -864,8 +536,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         const long long tw0 = wall_clock64();
 #endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (PW) wave_lds_sync();
-        else __syncthreads();
+        __syncthreads();
 #ifdef R3DG_EXP_COUNT
         t_wait += wall_clock64() - tw0;
 #endif
@@ -876,29 +547,22 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     if (l == 0) {
         R3DG_EXP_ADD(2, t_wait);                    // batch-end DMA wait + barrier, per wave
         R3DG_EXP_ADD(3, wall_clock64() - t_begin);  // batch loop total, per wave
-        R3DG_EXP_ADD(4, t_mask);                    // DMA issue + cull masks, per wave
+        R3DG_EXP_ADD(4, t_mask);                    // DMA issue + live masks, per wave
     }
 #endif
 }
 
 template <int SMAX>
 static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
-    // R3DG_BWD: "dpp" = DPP-reduction cross-check, "wave" = one 64-thread workgroup per (tile,
-    // quadrant) (measured 7 % slower at M1), "block" = one 256-thread workgroup per tile with
-    // register staging (2 barriers per batch, measured 2.7 % slower), default = the DMA-staged
-    // workgroup per tile (render_bwd_glds_kernel). All write the same partial rows.
-    const char* e = getenv("R3DG_BWD");
+    // R3DG_BWD=dpp: the DPP-reduction cross-check (tests/test_gpu_parity.py); default: the
+    // DMA-staged MFMA kernel. Both write the same partial rows (the forward's contribution set).
+    const char* e = getenv("R3DG_BWD");  // read per launch: tests switch it at run time
+    const bool dpp = e && e[0] == 'd';
     const int grid = padded_tile_grid(a.num_tiles);
-    if (e && e[0] == 'd')
+    if (dpp)
         launch_kernel(render_bwd_dpp_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
-    else if (e && e[0] == 'w')
-        launch_kernel(render_bwd_mfma_kernel<SMAX, true>, dim3(4 * grid), dim3(64), stream, a);
-    else if (e && e[0] == 'b')
-        launch_kernel(render_bwd_mfma_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
-    else if (e && e[0] == 'q')
-        launch_kernel(render_bwd_glds_kernel<SMAX, true>, dim3(4 * grid), dim3(64), stream, a);
     else
-        launch_kernel(render_bwd_glds_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
+        launch_kernel(render_bwd_glds_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
     return hipGetLastError();
 }
 
@@ -975,7 +639,7 @@ __device__ static void sh_backward(int deg, int M, float3 pos, const float* camp
     const int ncoef = deg > 2 ? 16 : (deg > 1 ? 9 : (deg > 0 ? 4 : 1));
     for (int i = 0; i < M; ++i)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) dsh[3 * i + c] = i < ncoef ? __fmul_rn(b[i], dRGB[c]) : 0.f;
+        for (int c = 0; c < 3; ++c) dsh[3 * i + c] = i < ncoef ? b[i] * dRGB[c] : 0.f;  // one rounding
     const float dvx = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
     const float dvy = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
     const float dvz = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
@@ -1166,6 +830,7 @@ __global__ void __launch_bounds__(256) sh_grad_views_kernel(int g0, int n, int d
                                                             const float* __restrict__ means3D,
                                                             const float* __restrict__ campos,
                                                             const float* __restrict__ drgb, float* __restrict__ dsh) {
+#pragma clang fp contract(off)  // the products and sums round separately, as sh_backward's (no FMA)
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const int g = g0 + i;
@@ -1176,16 +841,22 @@ __global__ void __launch_bounds__(256) sh_grad_views_kernel(int g0, int n, int d
     for (int k = 0; k < 16; ++k) acc[k][0] = acc[k][1] = acc[k][2] = 0.f;
     const float3 pos = make_float3(px, py, pz);
     for (int v = 0; v < N; ++v) {
-        float dox, doy, doz, x, y, z, b[16];
-        sh_dir_basis(pos, campos + 3 * v, dox, doy, doz, x, y, z, b);
         const float* d = drgb + ((size_t)v * n + i) * 3;
         const float d0 = d[0], d1 = d[1], d2 = d[2];
+        // a view without colour gradient adds nothing (the reference skips radii == 0,
+        // backward.cu:348-398); skipping also keeps a mean at that view's camera centre (0/0
+        // direction) from adding NaN * 0. Bitwise the same sums otherwise: acc + (+-0) == acc.
+        if (d0 == 0.f && d1 == 0.f && d2 == 0.f) continue;
+        float dox, doy, doz, x, y, z, b[16];
+        sh_dir_basis(pos, campos + 3 * v, dox, doy, doz, x, y, z, b);
         // each view's product rounded as sh_backward rounds it, then summed in view order
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            acc[k][0] = __fadd_rn(acc[k][0], __fmul_rn(b[k], d0));
-            acc[k][1] = __fadd_rn(acc[k][1], __fmul_rn(b[k], d1));
-            acc[k][2] = __fadd_rn(acc[k][2], __fmul_rn(b[k], d2));
+            // plain operators under this function's contract(off): the __fadd_rn / __fmul_rn helpers
+            // are header functions compiled with contraction on, so they fuse into an FMA
+            acc[k][0] = acc[k][0] + b[k] * d0;
+            acc[k][1] = acc[k][1] + b[k] * d1;
+            acc[k][2] = acc[k][2] + b[k] * d2;
         }
     }
     float* o = dsh + (size_t)g * M * 3;

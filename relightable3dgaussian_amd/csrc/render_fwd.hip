@@ -3,21 +3,18 @@
 // Restates reference forward.cu:388-561 (renderCUDA) with an MI355X layout:
 //   * one 256-thread workgroup per tile; each wave64 owns an 8x8 quadrant (square, so the
 //     per-wave footprint test below rejects more Gaussians than 16x4 strips would);
-//   * each batch of 256 sorted instances is staged in LDS once: xy, conic|opacity, and an AoS
-//     attribute row (colour, depth, [shader colour], features) read with ds_read_b128
-//     broadcasts -- the reference re-reads colours and features from HBM per pixel;
-//   * a conservative per-quadrant footprint mask (minimum of the conic form over the quadrant
-//     against the widened alpha >= 1/255 threshold, r3dg_common.h quadrant_mask) decides
-//     which instances a wave visits. Skipping is exact: a skipped instance would have failed
-//     the reference's alpha test on every pixel of the quadrant (tests/test_gpu_parity.py
-//     checks cull on == cull off bit for bit). The masks are compacted at staging time into
-//     per-wave 32-bit chunk masks (one ballot per wave), so a wave iterates only its live
-//     instances with s_ff1 -- no per-instance scalar test;
+//   * the render records of the next 64-instance batch are copied HBM -> LDS by LDS-DMA while the
+//     current batch blends (render_fwd_glds_kernel; one block barrier per batch, 8 waves/SIMD);
+//   * a conservative per-quadrant footprint test (minimum of the conic form over the quadrant
+//     against the widened alpha >= 1/255 threshold, r3dg_common.h rect_culled) decides which
+//     instances a wave visits. Skipping is exact: a skipped instance would have failed the
+//     reference's alpha test on every pixel of the quadrant (tests/test_gpu_parity.py checks cull
+//     on == cull off bit for bit, also on needle-shaped splats);
+//   * every wave records which staged instances at least one of its pixels blended: one byte
+//     per sorted position (bit = quadrant), the exact visit list of the backward (render_bwd.hip);
 //   * early exit per wave (ballot) and per block (__syncthreads_count), as the reference;
 //   * XCD-aware tile order (r3dg_kernels.h).
-// Default-shader path: render_fwd_glds_kernel stages the render records of the next 64-instance
-// batch by LDS-DMA while the current one blends (one barrier per batch, 8 waves/SIMD; M1 forward
-// 0.484 -> 0.447 ms); render_fwd_kernel stays for the splat shaders and as R3DG_FWD=ld.
+// render_fwd_shader_kernel blends the splat-shader colour as well (non-default splat shaders).
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
 
@@ -27,34 +24,28 @@ namespace r3dg {
 R3DG_EXP_READER(r3dg_exp_counters_fwd)
 #endif
 
-// Tuning knobs (experiment builds override them through R3DG_EXTRA_HIPFLAGS).
-#ifndef R3DG_FWD_NB
-#define R3DG_FWD_NB 256  // instances staged per batch
-#endif
 #ifndef R3DG_FWD_WAVES
 #define R3DG_FWD_WAVES 6  // waves per SIMD the register allocation targets (SMAX <= 12)
 #endif
-#ifndef R3DG_FWD_PRED
-#define R3DG_FWD_PRED 0  // 1: accumulation predicated (weight 0) instead of branched (measured slower)
-#endif
-#ifndef R3DG_FWD_PKEXP
-#define R3DG_FWD_PKEXP 1  // 1: a pair's two exps as packed f32 ops (bit-identical per component)
-#endif
-#ifndef R3DG_FWD_PAIR
-#define R3DG_FWD_PAIR 1  // two compacted instances per loop iteration
-#endif
 
-template <int SMAX, bool SHADER>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_FWD_WAVES : 1)))
-render_fwd_kernel(RenderFwdArgs a) {
-    constexpr int NB = R3DG_FWD_NB;
-    constexpr int FO = SHADER ? 8 : 4;                 // feature offset inside the attribute row
+// ---------------------------------------------------------------------------------------------
+// Splat-shader blend (a non-default splat shader is active): the per-Gaussian shader colour is not
+// part of the render record, so instances are staged from the SoA geometry state by registers,
+// 256 per batch, two block barriers per batch. Blends colour and shader colour with the same step
+// as render_fwd_glds_kernel and writes the same contribution bits.
+// ---------------------------------------------------------------------------------------------
+template <int SMAX>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? 4 : 1)))
+render_fwd_shader_kernel(RenderFwdArgs a) {
+    constexpr int NB = kBlock;                         // instances staged per batch
+    constexpr int FO = 8;                              // feature offset inside the attribute row
     constexpr int NA4 = (FO + SMAX + 3) / 4;           // float4 per attribute row
     __shared__ float2 s_xy[NB];
     __shared__ float4 s_co[NB];
     __shared__ float4 s_attr[NA4 * NB];                // q-major: float4 q of instance j at q*NB + j
                                                        // (staging writes 16-B strided: conflict-free)
     __shared__ uint32_t s_bits[NB / 32][4];            // [32-instance chunk][wave]: live-instance masks
+    __shared__ uint32_t s_cw[NB / 32][4];              // [chunk][wave]: contribution bits of the batch
 
     const int tile = block_tile(a.tile_order, a.num_tiles);
     if (tile >= a.num_tiles) return;
@@ -75,56 +66,54 @@ render_fwd_kernel(RenderFwdArgs a) {
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) F[c] = 0.f;
 
+    // contribution byte of instance t of the batch at b0 (render_fwd_glds_kernel's layout)
+    auto write_bits = [&](int b0, int cnt) {
+        if (t < cnt) {
+            const int c = t >> 5, sh = t & 31;
+            const uint32_t v = ((s_cw[c][0] >> sh) & 1u) | ((s_cw[c][1] >> sh) & 1u) << 1 |
+                               ((s_cw[c][2] >> sh) & 1u) << 2 | ((s_cw[c][3] >> sh) & 1u) << 3;
+            a.contrib[range.x + (uint32_t)(b0 + t)] = (uint8_t)v;
+        }
+    };
     // Gaussian ids loaded one batch ahead: staging waits for one dependent round trip, not two
-    uint32_t gid_next = (t < NB && t < n) ? a.point_list[range.x + t] : 0u;
-    for (int base = 0; base < n; base += NB) {
-        if (__syncthreads_count(done) == kBlock) break;
+    uint32_t gid_next = t < n ? a.point_list[range.x + t] : 0u;
+    int base = 0;
+    for (; base < n; base += NB) {
+        const bool all_done = __syncthreads_count(done) == kBlock;
+        if (base > 0) write_bits(base - NB, NB);  // s_cw is rewritten only after the next barrier
+        if (all_done) break;
         uint32_t m = 0;
-        if (t < NB && base + t < n) {
+        if (base + t < n) {
             const uint32_t gid = gid_next;
             gid_next = (base + NB + t < n) ? a.point_list[range.x + base + NB + t] : 0u;
-            if constexpr (!SHADER) {
-                // one contiguous render record per Gaussian (r3dg_kernels.h record_f4)
-                const float4* rec = a.records + (size_t)gid * (2 + NA4);
-                const float4 co = rec[0], r1 = rec[1];
-                const float2 xy = make_float2(r1.x, r1.y);
-                s_xy[t] = xy;
-                s_co[t] = co;
-                m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
+            const float2 xy = a.means2D[gid];
+            const float4 co = a.conic_opacity[gid];
+            s_xy[t] = xy;
+            s_co[t] = co;
+            m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
+            float v[NA4 * 4];
 #pragma unroll
-                for (int q = 0; q < NA4; ++q) s_attr[q * NB + t] = rec[2 + q];
-            } else {
-                const float2 xy = a.means2D[gid];
-                const float4 co = a.conic_opacity[gid];
-                s_xy[t] = xy;
-                s_co[t] = co;
-                m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
-                float v[NA4 * 4];
+            for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
+            v[0] = a.colors[3 * gid + 0];
+            v[1] = a.colors[3 * gid + 1];
+            v[2] = a.colors[3 * gid + 2];
+            v[3] = a.depths[gid];
+            v[4] = a.shader_colors[3 * gid + 0];
+            v[5] = a.shader_colors[3 * gid + 1];
+            v[6] = a.shader_colors[3 * gid + 2];
+            const float* f = a.features + (size_t)gid * a.S;
 #pragma unroll
-                for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
-                v[0] = a.colors[3 * gid + 0];
-                v[1] = a.colors[3 * gid + 1];
-                v[2] = a.colors[3 * gid + 2];
-                v[3] = a.depths[gid];
-                if constexpr (SHADER) {
-                    v[4] = a.shader_colors[3 * gid + 0];
-                    v[5] = a.shader_colors[3 * gid + 1];
-                    v[6] = a.shader_colors[3 * gid + 2];
-                }
-                const float* f = a.features + (size_t)gid * a.S;
+            for (int c = 0; c < SMAX; ++c)
+                if (c < a.S) v[FO + c] = f[c];
 #pragma unroll
-                for (int c = 0; c < SMAX; ++c)
-                    if (c < a.S) v[FO + c] = f[c];
-#pragma unroll
-                for (int q = 0; q < NA4; ++q)
-                    s_attr[q * NB + t] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-            }
+            for (int q = 0; q < NA4; ++q)
+                s_attr[q * NB + t] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
         }
         // compaction: this wave's 64 staged slots are chunks 2w and 2w+1; one ballot per target wave
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const unsigned long long bal = __ballot((m >> b) & 1u);
-            if (l == 0 && w < NB / 64) {
+            if (l == 0) {
                 s_bits[2 * w][b] = (uint32_t)bal;
                 s_bits[2 * w + 1][b] = (uint32_t)(bal >> 32);
             }
@@ -133,6 +122,7 @@ render_fwd_kernel(RenderFwdArgs a) {
         // One blend step of renderCUDA (forward.cu:470-520): the tests are predicated, every LDS
         // read of the instance is issued before them, and only the accumulation is a branch.
         // `power` and G = r3dg_expf(power) come from the caller (a pair's two exps run packed).
+        uint32_t cw = 0u;  // contribution bits of the current chunk
         auto step = [&](int j, bool live, float opacity, float power, float G) {
 #pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
             float v[NA4 * 4];
@@ -146,93 +136,53 @@ render_fwd_kernel(RenderFwdArgs a) {
             const float test_T = T * (1.0f - alpha);
             const bool stop = test_T < 0.0001f;
             done = done || (contrib && stop);
-#if R3DG_FWD_PRED
-            // predicated accumulation: a non-contributing pixel adds v * 0 (exact: C + +-0 == C), so
-            // the step is straight-line code and the paired steps' LDS reads overlap
-            {
-                const bool acc = contrib && !stop;
-                const float wgt = acc ? alpha * T : 0.f;
-                C[0] = __builtin_fmaf(v[0], wgt, C[0]);
-                C[1] = __builtin_fmaf(v[1], wgt, C[1]);
-                C[2] = __builtin_fmaf(v[2], wgt, C[2]);
-                if constexpr (SHADER) {
-                    CS[0] = __builtin_fmaf(v[4], wgt, CS[0]);
-                    CS[1] = __builtin_fmaf(v[5], wgt, CS[1]);
-                    CS[2] = __builtin_fmaf(v[6], wgt, CS[2]);
-                }
-#pragma unroll
-                for (int c2 = 0; c2 < SMAX; ++c2) F[c2] = __builtin_fmaf(v[FO + c2], wgt, F[c2]);
-                Dp = __builtin_fmaf(v[3], wgt, Dp);
-                Op += wgt;
-                T = acc ? test_T : T;
-                last = acc ? (uint32_t)(base + j + 1) : last;
-            }
-#else
+            if (__ballot(contrib && !stop) != 0ull) cw |= 1u << (__builtin_amdgcn_readfirstlane(j) & 31);
             if (contrib && !stop) {
                 const float wgt = alpha * T;
                 C[0] = __builtin_fmaf(v[0], wgt, C[0]);
                 C[1] = __builtin_fmaf(v[1], wgt, C[1]);
                 C[2] = __builtin_fmaf(v[2], wgt, C[2]);
-                if constexpr (SHADER) {
-                    CS[0] = __builtin_fmaf(v[4], wgt, CS[0]);
-                    CS[1] = __builtin_fmaf(v[5], wgt, CS[1]);
-                    CS[2] = __builtin_fmaf(v[6], wgt, CS[2]);
-                }
-#ifndef R3DG_EXP_NOACC  // timing experiment only: drop the feature accumulation
+                CS[0] = __builtin_fmaf(v[4], wgt, CS[0]);
+                CS[1] = __builtin_fmaf(v[5], wgt, CS[1]);
+                CS[2] = __builtin_fmaf(v[6], wgt, CS[2]);
 #pragma unroll
                 for (int c2 = 0; c2 < SMAX; ++c2) F[c2] = __builtin_fmaf(v[FO + c2], wgt, F[c2]);
-#endif
                 Dp = __builtin_fmaf(v[3], wgt, Dp);
                 Op += wgt;
                 T = test_T;
                 last = (uint32_t)(base + j + 1);
             }
-#endif
         };
         bool alive = __ballot(!done) != 0ull;
-        for (int c = 0; c < NB / 32 && alive; ++c) {
-            uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[c][w]);
-            if (l == 0) R3DG_EXP_ADD(3, __builtin_popcount(bits));
+        for (int c = 0; c < NB / 32; ++c) {
+            uint32_t bits = alive ? __builtin_amdgcn_readfirstlane(s_bits[c][w]) : 0u;
+            cw = 0u;
             while (bits) {
-#if R3DG_FWD_PAIR
                 // two compacted instances per iteration (the second one's reads overlap the first)
                 const int j0 = c * 32 + __builtin_ctz(bits);
                 bits &= bits - 1;
                 const bool has1 = bits != 0u;
                 const int j1 = has1 ? c * 32 + __builtin_ctz(bits) : j0;
                 bits &= bits - 1;
-                {
-                    // both exps at once (packed): neither depends on T
-                    const float4 co0 = s_co[j0], co1 = s_co[j1];
-                    const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
-                    const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
-                    const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
-#if R3DG_FWD_PKEXP
-                    const f32x2 G = r3dg_expf2(pw0, pw1);
-                    step(j0, true, co0.w, pw0, G.x);
-                    step(j1, has1, co1.w, pw1, G.y);
-#else
-                    step(j0, true, co0.w, pw0, r3dg_expf(pw0));
-                    step(j1, has1, co1.w, pw1, r3dg_expf(pw1));
-#endif
-                }
-                if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
-#else
-                const int j0 = c * 32 + __builtin_ctz(bits);
-                bits &= bits - 1;
-                {
-                    const float4 co0 = s_co[j0];
-                    const float2 xy0 = s_xy[j0];
-                    const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
-                    step(j0, true, co0.w, pw0, r3dg_expf(pw0));
-                }
-#endif
+                const float4 co0 = s_co[j0], co1 = s_co[j1];
+                const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
+                const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
+                const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
+                const f32x2 G = r3dg_expf2(pw0, pw1);  // both exps at once: neither depends on T
+                step(j0, true, co0.w, pw0, G.x);
+                step(j1, has1, co1.w, pw1, G.y);
                 if (__ballot(!done) == 0ull) {  // converged here: a uniform exit
                     alive = false;
                     break;
                 }
             }
+            if (l == 0) s_cw[c][w] = cw;
         }
+    }
+    if (base >= n && n > 0) {  // ran to the end: the last batch's bits (block-uniform)
+        __syncthreads();
+        const int b0 = (n - 1) / NB * NB;
+        write_bits(b0, n - b0);
     }
 
     if (inside) {
@@ -243,16 +193,9 @@ render_fwd_kernel(RenderFwdArgs a) {
         a.out_color[3 * pix + 0] = C[0] + T * b0;
         a.out_color[3 * pix + 1] = C[1] + T * b1;
         a.out_color[3 * pix + 2] = C[2] + T * b2;
-        if constexpr (SHADER) {
-            a.out_shader_color[3 * pix + 0] = CS[0] + T * b0;
-            a.out_shader_color[3 * pix + 1] = CS[1] + T * b1;
-            a.out_shader_color[3 * pix + 2] = CS[2] + T * b2;
-        } else {
-            // default splat shader: shader colour == SH colour (splatShader.cu:67-71)
-            a.out_shader_color[3 * pix + 0] = C[0] + T * b0;
-            a.out_shader_color[3 * pix + 1] = C[1] + T * b1;
-            a.out_shader_color[3 * pix + 2] = C[2] + T * b2;
-        }
+        a.out_shader_color[3 * pix + 0] = CS[0] + T * b0;
+        a.out_shader_color[3 * pix + 1] = CS[1] + T * b1;
+        a.out_shader_color[3 * pix + 2] = CS[2] + T * b2;
         a.out_depth[pix] = Dp;
         a.out_opacity[pix] = Op;
         if (a.zero_stencil) a.zero_stencil[pix] = 0.f;
@@ -263,13 +206,12 @@ render_fwd_kernel(RenderFwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Double-buffered variant of the default-shader blend (render records only): the records of batch
-// b+1 are copied HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no staging stores)
-// while the waves blend batch b, so the record round trip leaves the critical path and a batch
-// costs one block barrier (the early-exit count) instead of two. Every wave evaluates the exact
-// quadrant cull of the staged instances for its own quadrant (render_bwd_glds_kernel does the
-// same). Staging layout: column q (float4 q of the render record) of instance j at [q * NB + j].
-// Same blend step, same decisions and sums as render_fwd_kernel (bitwise).
+// The default-shader blend (render records only): the records of batch b+1 are copied HBM -> LDS
+// by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no staging stores) while the waves blend batch b,
+// so the record round trip leaves the critical path and a batch costs one block barrier (the
+// early-exit count). Every wave evaluates the exact quadrant cull of the staged instances for its
+// own quadrant. Staging layout: column q (float4 q of the render record) of instance j at
+// [q * NB + j]. Same blend step, same decisions and sums as render_fwd_shader_kernel (bitwise).
 // ---------------------------------------------------------------------------------------------
 #ifndef R3DG_FWDG_NB
 #define R3DG_FWDG_NB 64  // instances per staged batch (two resident: 12.3 KB, 64 VGPRs -> 8 waves/SIMD;
@@ -285,8 +227,11 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     constexpr int RF4 = 2 + NA4;               // float4 per render record
     constexpr int SBUF = RF4 * NB;             // float4 per staging buffer
     constexpr int NCP = RF4 * NH;              // DMA wave-instructions per batch
-    static_assert(NB % 64 == 0 && NB <= 256, "a DMA wave-instruction covers 64 instances of one column");
-    __shared__ float4 s_lds[2 * SBUF];
+    static_assert(NB == 64, "one 64-bit contribution word per wave and batch");
+    // one LDS array: [2 staging buffers | 2 x 64 x 4 contribution flags (batch buffer, instance, wave)]
+    __shared__ float4 s_lds[2 * SBUF + 32];
+    uint8_t* const s_cf = reinterpret_cast<uint8_t*>(s_lds + 2 * SBUF);
+    if (threadIdx.x < 128) reinterpret_cast<uint32_t*>(s_cf)[threadIdx.x] = 0u;  // before the first barrier
 
     const int tile = block_tile(a.tile_order, a.num_tiles);
     if (tile >= a.num_tiles) return;
@@ -338,11 +283,30 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         if (n > NB) load_gids(NB, gnext);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // Contribution bits for the backward (render_bwd.hip): the byte of sorted position p holds bit
+    // q when a pixel of quadrant q blended instance p. Every accumulating lane of wave w sets the LDS
+    // flag byte [batch buffer][instance][w] (all write the same 1: no per-step ballot or scalar
+    // work); after the next batch barrier wave 0 folds each instance's four flag bytes into the
+    // contribution byte, stores it and clears the flags for their reuse two batches on.
+    // Positions past a block's early exit are never written: the backward only visits positions
+    // below the tile's largest n_contrib.
+    auto write_bits = [&](int b0, int cnt, int bb) {
+        if (w == 0 && l < cnt) {
+            uint32_t* f = reinterpret_cast<uint32_t*>(s_cf) + 64 * bb + l;
+            const uint32_t fw = *f;
+            *f = 0u;
+            const uint32_t v = (fw & 1u) | (fw >> 7 & 2u) | (fw >> 14 & 4u) | (fw >> 21 & 8u);
+            a.contrib[range.x + (uint32_t)(b0 + l)] = (uint8_t)v;
+        }
+    };
     int buf = 0;
-    for (int base = 0; base < n; base += NB) {
+    int base = 0;
+    for (; base < n; base += NB) {
         // batch `base` has landed (every wave waited for its own DMA) and nobody reads the other
         // buffer any more
-        if (__syncthreads_count(done) == kBlock) break;
+        const bool all_done = __syncthreads_count(done) == kBlock;
+        if (base > 0) write_bits(base - NB, NB, buf ^ 1);  // the previous batch's flags
+        if (all_done) break;
         if (base + NB < n) {  // block-uniform: stage the next batch while this one blends
             issue(gnext, buf ^ 1);
             if (base + 2 * NB < n) load_gids(base + 2 * NB, gnext);
@@ -374,6 +338,15 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
             const float test_T = T * (1.0f - alpha);
             const bool stop = test_T < 0.0001f;
             done = done || (contrib && stop);
+#ifdef R3DG_EXP_COUNT
+            {
+                const unsigned long long acc_b = __ballot(contrib && !stop);
+                if (l == 0) {
+                    R3DG_EXP_ADD(4, __builtin_popcountll(acc_b));
+                    R3DG_EXP_ADD(5, acc_b != 0ull ? 1 : 0);
+                }
+            }
+#endif
             if (contrib && !stop) {
                 const float wgt = alpha * T;
                 C[0] = __builtin_fmaf(v[0], wgt, C[0]);
@@ -385,6 +358,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 Op += wgt;
                 T = test_T;
                 last = (uint32_t)(base + j + 1);
+                s_cf[(buf * 64 + ju) * 4 + w] = 1;  // every accumulating lane writes the same byte
             }
         };
         bool alive = __ballot(!done) != 0ull;
@@ -415,6 +389,11 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         buf ^= 1;
     }
     // a block that stops early has no DMA in flight: every issued batch was waited for above
+    if (base >= n && n > 0) {  // ran to the end: the last batch's bits are still in LDS (block-uniform)
+        __syncthreads();
+        const int b0 = (n - 1) / NB * NB;
+        write_bits(b0, n - b0, buf ^ 1);
+    }
 
     if (inside) {
         const int pix = py * a.W + px;
@@ -440,16 +419,9 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
 
 template <int SMAX>
 static hipError_t launch_fwd_s(const RenderFwdArgs& a, bool shader, hipStream_t stream) {
-    // R3DG_FWD=ld: the register-staged kernel for the default shader too (cross-check / A-B)
-    static const bool use_ld = [] {
-        const char* e = getenv("R3DG_FWD");
-        return e && e[0] == 'l';
-    }();
     const int grid = padded_tile_grid(a.num_tiles);
     if (shader)
-        launch_kernel(render_fwd_kernel<SMAX, true>, dim3(grid), dim3(kBlock), stream, a);
-    else if (use_ld || !a.records)
-        launch_kernel(render_fwd_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
+        launch_kernel(render_fwd_shader_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
     else
         launch_kernel(render_fwd_glds_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
     return hipGetLastError();

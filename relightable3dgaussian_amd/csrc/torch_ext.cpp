@@ -293,8 +293,13 @@ torch::Tensor sh_color_grads(const torch::Tensor& geomBuffer, int64_t P, const t
                              int64_t g1) {
     const torch::Device dev = dL_dcolors.device();
     const c10::OptionalDeviceGuard guard(dev);
-    TORCH_CHECK(dev.is_cuda() && dL_dcolors.is_contiguous() && dL_dcolors.numel() == 3 * P && 0 <= g0 && g0 <= g1 &&
-                    g1 <= P, "sh_color_grads: dL_dcolors must be a contiguous CUDA [P,3] tensor, 0 <= g0 <= g1 <= P");
+    TORCH_CHECK(dev.is_cuda() && dL_dcolors.is_contiguous() && dL_dcolors.scalar_type() == torch::kFloat32 &&
+                    dL_dcolors.numel() == 3 * P && 0 <= g0 && g0 <= g1 && g1 <= P,
+                "sh_color_grads: dL_dcolors must be a contiguous float32 CUDA [P,3] tensor, 0 <= g0 <= g1 <= P");
+    TORCH_CHECK(geomBuffer.device() == dev && geomBuffer.is_contiguous() &&
+                    (size_t)geomBuffer.nbytes() >= r3dg_geom_state_bytes((int)P, -1),
+                "sh_color_grads: geomBuffer must be the forward's geometry state for these P Gaussians, on the "
+                "gradients' device");
     auto out = torch::empty({g1 - g0, 3}, dL_dcolors.options());
     check(r3dg_sh_color_grads((int)P, (int)g0, (int)(g1 - g0), geomBuffer.data_ptr(), dL_dcolors.data_ptr<float>(),
                               out.data_ptr<float>(), stream_of(dev)),
@@ -312,6 +317,12 @@ void sh_grad_from_views(const torch::Tensor& means3D, const torch::Tensor& campo
                     campos.size(0) == drgb.size(0) && dL_dsh.dim() == 3 && dL_dsh.size(2) == 3 &&
                     dL_dsh.is_contiguous() && g0 >= 0 && g0 + drgb.size(1) <= dL_dsh.size(0),
                 "sh_grad_from_views: drgb [N,n,3], campos [N,3], dL_dsh [P,M,3] contiguous");
+    TORCH_CHECK(means3D.dim() == 2 && means3D.size(1) == 3 && means3D.size(0) >= g0 + drgb.size(1),
+                "sh_grad_from_views: means3D must be [P,3] with P >= g0 + n");
+    TORCH_CHECK(dL_dsh.device() == dev && dL_dsh.scalar_type() == torch::kFloat32 && dL_dsh.size(1) <= 16 &&
+                    degree >= 0 && degree <= 3 && (degree + 1) * (degree + 1) <= dL_dsh.size(1),
+                "sh_grad_from_views: dL_dsh must be a float32 [P,M,3] tensor on means3D's device, degree 0..3 with "
+                "(degree+1)^2 <= M <= 16");
     auto m3 = dev_contig(means3D, dev), cp = dev_contig(campos, dev), d = dev_contig(drgb, dev);
     check(r3dg_sh_grad_from_views((int)g0, (int)drgb.size(1), (int)degree, (int)dL_dsh.size(1), (int)drgb.size(0),
                                   m3.data_ptr<float>(), cp.data_ptr<float>(), d.data_ptr<float>(),

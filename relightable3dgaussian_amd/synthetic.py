@@ -171,6 +171,37 @@ def ball_scene(P: int = 300_000, S: int = 21, seed: int = 0, radius: float = 1.3
     return Scene(means, scales, rot, opacity, sh, feats)
 
 
+def needle_scene(P: int = 300, S: int = 11, seed: int = 0, cam: Camera | None = None,
+                 sigma_px=(100.0, 1000.0), opacity=(0.005, 0.05)) -> Scene:
+    """Adversarial scene for the quadrant cull (r3dg_common.h quadrant_live): large, needle-shaped,
+    faint splats on the screen diagonals, as trained scenes hold in their backgrounds. For the
+    M1 camera (identity rotation, +z forward): the long axis has a screen-space sigma log-uniform
+    in `sigma_px`, at 45 or 135 degrees (+-2); the two short axes are 1e-6 world units, so the 2D
+    covariance's short axis is the 0.3 px^2 low-pass floor (forward.cu:110-111); opacity uniform
+    in `opacity`; means projected anywhere in [-600, W+600] x [-600, H+600] px, mostly far from
+    the tiles the splat covers. The conic form's terms reach ~1e6 along the needle and cancel to
+    a few units: the regime where a fixed cull margin is smaller than the fp32 rounding."""
+    cam = cam or m1_camera()
+    rng = np.random.default_rng(seed)
+    fx, fy = cam.focal
+    z = rng.uniform(3, 8, P)
+    u = rng.uniform(-600, cam.width + 600, P)
+    v = rng.uniform(-600, cam.height + 600, P)
+    means = np.stack([(u - cam.cx) / fx * z, (v - cam.cy) / fy * z, z], 1).astype(np.float32)
+    sig = np.exp(rng.uniform(np.log(sigma_px[0]), np.log(sigma_px[1]), P))
+    scales = np.full((P, 3), 1e-6, np.float64)
+    scales[:, 0] = sig * z / fx
+    theta = np.radians(np.where(rng.uniform(size=P) < 0.5, 45.0, 135.0) + rng.uniform(-2, 2, P))
+    rot = np.zeros((P, 4))
+    rot[:, 0], rot[:, 3] = np.cos(theta / 2), np.sin(theta / 2)  # (w, x, y, z): about the view axis
+    op = rng.uniform(opacity[0], opacity[1], (P, 1)).astype(np.float32)
+    sh = np.empty((P, 16, 3), np.float32)
+    sh[:, 0] = (rng.uniform(0, 1, (P, 3)) - 0.5) / 0.28209479
+    sh[:, 1:] = rng.normal(0, 0.05, (P, 15, 3))
+    feats = rng.uniform(0, 1, (P, S)).astype(np.float32)
+    return Scene(means, scales.astype(np.float32), rot.astype(np.float32), op, sh, feats)
+
+
 def small_scene(P: int = 2000, S: int = 11, seed: int = 0, width: int = 64, height: int = 48,
                 scale_range=(0.02, 0.2)) -> tuple[Scene, Camera]:
     """Small parity scene: an M1-style frustum fill at a size the CPU oracle finishes in seconds."""

@@ -14,7 +14,7 @@ def tt(a, device="cuda"):
 
 def hip_forward(_C, scene, cam, S=None, degree=3, bg=(1.0, 1.0, 1.0), use_sh=True, use_cov=False, colors=None,
                 scale_modifier=1.0, pseudo_normal=True, features=None, time=0.0, texture_manager=None,
-                sh_manager=None, splat_manager=None, post_passes=None):
+                sh_manager=None, splat_manager=None, post_passes=None, prefiltered=False):
     """Call _C.rasterize_gaussians with the argument order of rasterize_points.cu:39-71."""
     import torch
 
@@ -35,7 +35,7 @@ def hip_forward(_C, scene, cam, S=None, degree=3, bg=(1.0, 1.0, 1.0), use_sh=Tru
         tt(bg), time, 0.0, args["means3D"], args["features"], args["colors"], args["opacity"], args["scales"],
         args["rotations"], scale_modifier, args["cov3D"], tt(cam.view), tt(cam.view_inv), tt(cam.proj),
         tt(cam.proj_inv), cam.tanfovx, cam.tanfovy, cam.cx, cam.cy, cam.height, cam.width, args["sh"], degree,
-        tt(cam.campos), False, pseudo_normal, texture_manager, sh_manager, splat_manager, post_passes,
+        tt(cam.campos), prefiltered, pseudo_normal, texture_manager, sh_manager, splat_manager, post_passes,
         False)
     names = ["num_rendered", "n_contrib", "color", "opacity", "depth", "stencil", "feature", "shader_color", "normal",
              "surface_xyz", "radii", "geom", "binning", "image"]

@@ -2,6 +2,7 @@
 the whole frame, not a crop (the oracle runs one M1 fwd+bwd in ~20 s).
 
   * M1 -- the metric config: 1M Gaussians, 1920x1080, S = 11 (bench.py's workload);
+  * C4 -- the truck stand-in: 2M Gaussians, 1920x1080, S = 11 (long tiles: the 2048-instance sorter);
   * C2 -- the lego-eval stand-in: 300k Gaussians in a ball, 800x800 orbit camera, S = 21 in the
     reference's 21-channel block layout (forward.cu:537-558), fwd + bwd.
 
@@ -15,7 +16,7 @@ import pytest
 
 import oracle
 from relightable3dgaussian_amd import synthetic
-from tests._helpers import assert_close, hip_backward, hip_forward, upstream_grads
+from tests._helpers import assert_close, hip_backward, hip_forward, tt, upstream_grads
 from tests.test_gpu_parity import _check_forward, _grad_tol, _oracle_fwd
 
 pytestmark = pytest.mark.gpu
@@ -44,6 +45,24 @@ def test_m1_full_frame_parity(hip_ext):
     assert 4_000_000 < o["num_rendered"] < 6_500_000
     # a frame that saturates: the early stop (T < 1e-4) decides n_contrib on many pixels
     assert float((o["final_T"] < 1e-3).mean()) > 0.1
+
+
+@pytest.mark.timeout(900)
+def test_c4_full_frame_parity(hip_ext):
+    """C4 (Tanks&Temples truck stand-in, BASELINE.json configs[3]): the M1 generator at P = 2M,
+    1920x1080, S = 11. Its tiles average ~1,230 instances (max 1,587), so most of them take the
+    2048-instance sorter of the per-tile depth sort (preprocess.hip tile_depth_sort_kernel), the
+    stand-in for the reference's 45-bit SortPairs (rasterizer_impl.cu:366-374): keys, point_list and
+    ranges bit-exact against the oracle's stable sort, n_contrib / final_T bit-exact, images within
+    1e-4, gradients at the usual bar, on the whole frame."""
+    cam = synthetic.m1_camera()
+    scene = synthetic.m1_scene(P=2_000_000, S=11, seed=0, cam=cam)
+    o = _full_check(hip_ext, scene, cam, 11, (1.0, 1.0, 1.0))
+    assert 9_000_000 < o["num_rendered"] < 11_000_000
+    counts = o["ranges"][:, 1].astype(np.int64) - o["ranges"][:, 0]
+    # most tiles hold 1025..2048 instances: one 2048-chunk of the long-tile sorter each (merge
+    # rounds are covered by test_gpu_parity.py test_dense_tiles_depth_sort)
+    assert (counts > 1024).mean() > 0.5 and counts.max() <= 2048
 
 
 def test_c2_s21_full_frame_parity(hip_ext):
@@ -81,3 +100,72 @@ def test_c3_training_step_full_size(hip_ext):
         ref = ob[k]
         tol = (5e-4 if k == "env" else 2e-5) * max(float(np.abs(ref).max()), 1e-9)
         assert_close("d_" + k, v.cpu().numpy(), ref, tol, 1e-3)
+
+
+@pytest.mark.timeout(600)
+def test_c5_views_exchange_rehearsal(hip_ext):
+    """C5 (BASELINE.json configs[4]: an 8-camera lego batch, one view per GPU, per-Gaussian
+    gradients summed over xGMI) rehearsed in one process on one GPU: the C2 scene at full size
+    (300k Gaussians, 800x800, S = 21), C5's 8 orbit cameras (azimuth 45 deg * k, elevation 30 deg).
+    Every view runs rasterize_gaussians + rasterize_gaussians_backward; the "views" exchange
+    (view_parallel.py) is then replayed on the gathered data: each view's clamp-masked colour
+    gradient (r3dg_sh_color_grads) and camera centre go to r3dg_sh_grad_from_views, whose rebuilt
+    SH gradient must equal the sequential sum of the 8 per-view dL_dsh bit for bit.
+    View 0 is also checked against the oracle (the per-view parity the sum rests on)."""
+    import torch
+
+    from oracle import view_exchange
+
+    scene = synthetic.ball_scene(300_000, S=21, seed=0)
+    P = scene.P
+    dsh_sum = None
+    drgb, cams = [], []
+    for k in range(8):
+        cam = synthetic.orbit_camera(45.0 * k, 30.0, 4.0311, 0.6911112, 800, 800)
+        h = hip_forward(hip_ext, scene, cam, S=21)
+        dc, do, dd, df = upstream_grads(cam.height, cam.width, 21, seed=100 + k)
+        g = hip_backward(hip_ext, h, dc, do, dd, df)
+        if k == 0:
+            o = _oracle_fwd(scene, cam, 21)
+            _check_forward(h, o, 21)
+            go = oracle.rasterize_backward(o, dc, do, dd, df)
+            for name in ["dL_dcolors", "dL_dsh", "dL_dmeans3D", "dL_dopacity"]:
+                assert_close(name, g[name], go[name], _grad_tol(go[name]), 2e-3)
+            # the exchanged colour gradient is the oracle's, clamp-masked the same way
+            d0 = hip_ext.sh_color_grads(h["geom"], P, tt(g["dL_dcolors"]), 0, P).cpu().numpy()
+            np.testing.assert_array_equal(d0, view_exchange.sh_color_grads(g["dL_dcolors"], o["clamped"]))
+        drgb.append(hip_ext.sh_color_grads(h["geom"], P, tt(g["dL_dcolors"]), 0, P))
+        cams.append(np.asarray(cam.campos, np.float32))
+        dsh_sum = g["dL_dsh"].copy() if dsh_sum is None else dsh_sum + g["dL_dsh"]  # view order
+        del h
+    out = torch.full((P, 16, 3), float("nan"), device="cuda")
+    d_all = torch.stack(drgb)
+    half = (P // 2 + 255) // 256 * 256  # two chunks, as the chunked exchange delivers them
+    for g0, g1 in [(0, half), (half, P)]:
+        hip_ext.sh_grad_from_views(tt(scene.means3D), tt(np.stack(cams)), d_all[:, g0:g1].contiguous(), 3, g0, out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), dsh_sum)
+
+
+def test_c2_brdf_complex_full_size(hip_ext):
+    """C2's render_equation_forward_complex (the lego eval BRDF, neilf.py:96-170) on all 300k
+    Gaussians, 24 samples, degree-3 light SH: every output against the oracle at the small-size
+    bars of test_brdf_complex_matches_oracle_and_golden."""
+    from tests.test_gpu_parity import _brdf_tensors
+
+    P = 300_000
+    inp = synthetic.brdf_inputs(P, seed=11)
+    out = hip_ext.render_equation_forward_complex(*_brdf_tensors(inp), 24)
+    names = ["pbr", "incident_dirs", "incident_lights", "local_incident_lights", "global_incident_lights",
+             "incident_visibility", "diffuse_light", "local_diffuse_light", "accum", "rgb_d", "rgb_s"]
+    h = {k: v.cpu().numpy() for k, v in zip(names, out)}
+    o = oracle.brdf_forward_complex(inp, 24)
+    for k in names:
+        d = np.abs(h[k].astype(np.float64) - o[k])
+        excess = d - (2e-5 + 1e-4 * np.abs(o[k].astype(np.float64)))
+        if (excess > 0).any():
+            for idx in np.argsort(excess.reshape(-1))[::-1][:5]:
+                u = np.unravel_index(idx, d.shape)
+                print(f"{k}{tuple(int(x) for x in u)}: hip {h[k][u]:.7g} oracle {o[k][u]:.7g} "
+                      f"rough {float(inp['rough'][u[0], 0]):.4f}")
+        assert_close(k, h[k], o[k], 2e-5, 1e-4)

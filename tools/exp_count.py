@@ -23,3 +23,5 @@ print(f"bwd mask/issue ticks: {buf[4]} ({buf[4] / max(buf[3], 1):.3f})")
 # bench.main runs the warm-up steps, the timed steps and as many profiled steps: 2 at --steps 1
 print("m1 steps run: 2")
 print(f"fwd steps done: {fb[2]}\nfwd live pairs (pre-exit): {fb[3]}")
+print(f"fwd accumulated lane-steps: {fb[4]}\nfwd instances with any accumulating pixel: {fb[5]}")
+print(f"bwd visited instances with any ok pixel: {buf[5]} of {buf[0]}\nbwd ok lane-steps: {buf[6]}")

@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU call: bench A/B over (variant, lib dir) pairs: bash tools/gpu_ab2.sh TAG VARIANT:LIBDIR ...
-# VARIANT "-" = default backward, LIBDIR "-" = in-tree lib. Backward parity tests run per pair.
+# VARIANT "-" = default backward ("dpp" = the DPP cross-check), LIBDIR "-" = in-tree lib. Backward
+# parity tests run per pair.
 set -e
 TAG=$1; shift
 OUT=gpurun_out/$TAG

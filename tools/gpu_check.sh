@@ -5,7 +5,7 @@ set -e
 TAG=${1:-latest}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 echo "pytest ok"
 timeout -k 10 300 python bench.py > $OUT/bench.log 2>&1
 echo "bench ok"; tail -1 $OUT/bench.log
