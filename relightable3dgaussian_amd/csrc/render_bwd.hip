@@ -826,48 +826,62 @@ __global__ void __launch_bounds__(256) sh_color_grads_kernel(int n, const uint8_
 
 // One thread per Gaussian: the SH basis of each view's direction exactly as sh_backward computes
 // it (backward.cu:20-139), summed over the views in order.
-__global__ void __launch_bounds__(256) sh_grad_views_kernel(int g0, int n, int deg, int M, int N,
-                                                            const float* __restrict__ means3D,
-                                                            const float* __restrict__ campos,
-                                                            const float* __restrict__ drgb, float* __restrict__ dsh) {
+// One thread per Gaussian, 128 per workgroup; the block's [128, M, 3] output is assembled in LDS
+// and written as one contiguous span (a thread's own 192-byte row would be 64 lines per store).
+constexpr int kShViewsBlock = 128;
+__global__ void __launch_bounds__(kShViewsBlock) sh_grad_views_kernel(int g0, int n, int deg, int M, int N,
+                                                                     const float* __restrict__ means3D,
+                                                                     const float* __restrict__ campos,
+                                                                     const float* __restrict__ drgb,
+                                                                     float* __restrict__ dsh) {
 #pragma clang fp contract(off)  // the products and sums round separately, as sh_backward's (no FMA)
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const int g = g0 + i;
-    const float px = means3D[3 * g], py = means3D[3 * g + 1], pz = means3D[3 * g + 2];
-    const int ncoef = deg > 2 ? 16 : (deg > 1 ? 9 : (deg > 0 ? 4 : 1));
-    float acc[16][3];
+    constexpr int SHS = 49;     // LDS stride of one Gaussian's row (odd: conflict-free)
+    __shared__ float s_out[kShViewsBlock * SHS];
+    const int t = threadIdx.x;
+    const int ib = blockIdx.x * kShViewsBlock;
+    const int i = ib + t;
+    if (i < n) {
+        const int g = g0 + i;
+        const float3 pos = make_float3(means3D[3 * g], means3D[3 * g + 1], means3D[3 * g + 2]);
+        const int ncoef = deg > 2 ? 16 : (deg > 1 ? 9 : (deg > 0 ? 4 : 1));
+        float acc[16][3];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc[k][0] = acc[k][1] = acc[k][2] = 0.f;
-    const float3 pos = make_float3(px, py, pz);
-    for (int v = 0; v < N; ++v) {
-        const float* d = drgb + ((size_t)v * n + i) * 3;
-        const float d0 = d[0], d1 = d[1], d2 = d[2];
-        // a view without colour gradient adds nothing (the reference skips radii == 0,
-        // backward.cu:348-398); skipping also keeps a mean at that view's camera centre (0/0
-        // direction) from adding NaN * 0. Bitwise the same sums otherwise: acc + (+-0) == acc.
-        if (d0 == 0.f && d1 == 0.f && d2 == 0.f) continue;
-        float dox, doy, doz, x, y, z, b[16];
-        sh_dir_basis(pos, campos + 3 * v, dox, doy, doz, x, y, z, b);
-        // each view's product rounded as sh_backward rounds it, then summed in view order
+        for (int k = 0; k < 16; ++k) acc[k][0] = acc[k][1] = acc[k][2] = 0.f;
+        for (int v = 0; v < N; ++v) {
+            const float* d = drgb + ((size_t)v * n + i) * 3;
+            const float d0 = d[0], d1 = d[1], d2 = d[2];
+            // a view without colour gradient adds nothing (the reference skips radii == 0,
+            // backward.cu:348-398); skipping also keeps a mean at that view's camera centre (0/0
+            // direction) from adding NaN * 0. Bitwise the same sums otherwise: acc + (+-0) == acc.
+            if (d0 == 0.f && d1 == 0.f && d2 == 0.f) continue;
+            float dox, doy, doz, x, y, z, b[16];
+            sh_dir_basis(pos, campos + 3 * v, dox, doy, doz, x, y, z, b);
+            // each view's product rounded as sh_backward rounds it, then summed in view order
+            // (plain operators under this function's contract(off): the __fadd_rn / __fmul_rn
+            // helpers are header functions compiled with contraction on, so they would fuse)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            // plain operators under this function's contract(off): the __fadd_rn / __fmul_rn helpers
-            // are header functions compiled with contraction on, so they fuse into an FMA
-            acc[k][0] = acc[k][0] + b[k] * d0;
-            acc[k][1] = acc[k][1] + b[k] * d1;
-            acc[k][2] = acc[k][2] + b[k] * d2;
+            for (int k = 0; k < 16; ++k) {
+                acc[k][0] = acc[k][0] + b[k] * d0;
+                acc[k][1] = acc[k][1] + b[k] * d1;
+                acc[k][2] = acc[k][2] + b[k] * d2;
+            }
         }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (k < M) {
+                const bool on = k < ncoef;
+                s_out[t * SHS + 3 * k] = on ? acc[k][0] : 0.f;
+                s_out[t * SHS + 3 * k + 1] = on ? acc[k][1] : 0.f;
+                s_out[t * SHS + 3 * k + 2] = on ? acc[k][2] : 0.f;
+            }
     }
-    float* o = dsh + (size_t)g * M * 3;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if (k < M) {
-            const bool on = k < ncoef;
-            o[3 * k] = on ? acc[k][0] : 0.f;
-            o[3 * k + 1] = on ? acc[k][1] : 0.f;
-            o[3 * k + 2] = on ? acc[k][2] : 0.f;
-        }
+    __syncthreads();
+    const int M3 = 3 * M, ng = min(kShViewsBlock, n - ib);
+    float* o = dsh + (size_t)(g0 + ib) * M3;
+    for (int f = t; f < ng * M3; f += kShViewsBlock) {
+        const int gg = f / M3;
+        o[f] = s_out[gg * SHS + (f - gg * M3)];
+    }
 }
 
 hipError_t launch_sh_color_grads(int n, const uint8_t* clamped, const float* dcol, float* out, hipStream_t st) {
@@ -878,7 +892,8 @@ hipError_t launch_sh_color_grads(int n, const uint8_t* clamped, const float* dco
 hipError_t launch_sh_grad_views(int g0, int n, int deg, int M, int N, const float* means3D, const float* campos,
                                 const float* drgb, float* dsh, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sh_grad_views_kernel, dim3((n + 255) / 256), dim3(256), 0, st, g0, n, deg, M, N, means3D,
+    hipLaunchKernelGGL(sh_grad_views_kernel, dim3((n + kShViewsBlock - 1) / kShViewsBlock), dim3(kShViewsBlock), 0, st,
+                       g0, n, deg, M, N, means3D,
                        campos, drgb, dsh);
     return hipGetLastError();
 }

@@ -382,7 +382,9 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 step(j0, true, co0.w, pw0, G.x);
                 step(j1, has1, co1.w, pw1, G.y);
                 if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
-                if (__ballot(!done) == 0ull) alive = false;  // converged here: a uniform exit
+                // converged here: a uniform exit (testing every 2 or 4 iterations instead, which
+                // drops ~10 scalar instructions per iteration, measured no faster)
+                if (__ballot(!done) == 0ull) alive = false;
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

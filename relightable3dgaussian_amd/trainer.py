@@ -197,8 +197,11 @@ class GaussianTrainState:
         self.lrs[[n for n, _ in self.groups].index("xyz")] = float(lr)
         return lr
 
-    def step(self, adam_fn=None):
-        """optimizer.step() + zero_grad() (gaussian_model.py:615-617); sharded over ranks."""
+    def step(self, adam_fn=None, zero_grad: bool = False):
+        """optimizer.step() + zero_grad(set_to_none=True) (gaussian_model.py:615-617); sharded over
+        ranks. As with the reference's set-to-None gradients, the next step's gradients are written
+        (grad_view(name).copy_ / the backward's outputs), not accumulated, so the buffer is not
+        cleared; pass zero_grad=True when the caller accumulates into it."""
         import torch.distributed as dist
 
         from . import _C
@@ -219,7 +222,8 @@ class GaussianTrainState:
         if self.dist.world > 1:
             dist.all_gather_into_tensor(self.param, self.param[self.dist.rank * s:(self.dist.rank + 1) * s].clone(),
                                         group=self.dist.group)
-        self.grad.zero_()
+        if zero_grad:
+            self.grad.zero_()
 
     # ---- densification (train.py:170-186, gaussian_model.py:1025-1062) ------------------------
     def add_densification_stats(self, dL_dmeans2D, radii, normal_grad=None):

@@ -173,7 +173,7 @@ def chunk_views_hook(_C, works: list, gathered: list, geom, P: int, group=None, 
             if sh_on:
                 buf = torch.empty((world, g1 - g0, 3), dtype=d.dtype, device=d.device)
                 works.append(_all_gather_into(buf, d, group))
-                gathered.append((g0, buf, d))
+                gathered.append((g0, buf, d, len(works)))  # the chunk's exchange = works[:len]
 
     return hook
 
@@ -200,12 +200,18 @@ def backward_all_reduce(_C, bwd_args, n_chunks: int = 4, group=None, sh_exchange
         cams = gather_campos(campos, group)
         hook = chunk_views_hook(_C, works, gathered, geom, means3D.shape[0], group)
     grads = _C.rasterize_gaussians_backward_chunked(*bwd_args, n_chunks, hook)
-    for w in works:
-        w.wait()
     cur = torch.cuda.current_stream()
-    for g0, buf, _ in gathered:  # every rank rebuilds the same SH gradient sum
+    done = 0
+    for g0, buf, _, upto in gathered:
+        # every rank rebuilds the same SH gradient sum, chunk by chunk: a chunk's rebuild waits for
+        # that chunk's collectives only and overlaps the later chunks' communication
+        for w in works[done:upto]:
+            w.wait()
+        done = upto
         _C.sh_grad_from_views(means3D, cams, buf, degree, g0, grads[SH_INDEX])
         buf.record_stream(cur)  # allocated on the communication stream, read here
+    for w in works[done:]:
+        w.wait()
     return grads
 
 
