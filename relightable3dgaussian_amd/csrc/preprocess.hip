@@ -381,7 +381,9 @@ __global__ void __launch_bounds__(kSortBT) __attribute__((amdgpu_waves_per_eu(8)
     const uint32_t s = rg.x, n = rg.y - rg.x;
     if (n <= 1) return;
     const int t = threadIdx.x;
-    const uint32_t kChunk = n <= kSortBT * 4 ? kSortBT * 4 : kSortBT * R3DG_SORT_LONG_IPT;  // block-uniform
+    // sorter capacity by tile length (block-uniform); a 2-item sorter for tiles of up to 512
+    // instances measured no faster (M1: 0.086 vs 0.083 ms, it spills one VGPR)
+    const uint32_t kChunk = n <= kSortBT * 4 ? kSortBT * 4 : kSortBT * R3DG_SORT_LONG_IPT;
     const uint32_t nchunks = (n + kChunk - 1) / kChunk;
     int rounds = 0;
     while ((1u << rounds) < nchunks) ++rounds;

@@ -370,6 +370,10 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 
     auto flush = [&](int r) {
         if (l == 0) R3DG_EXP_ADD(1, 1);
+#ifdef R3DG_EXP_NOFLUSH  // timing experiment only (results invalid): no reduction, no rows
+        (void)r;
+        return;
+#endif
         float yA[2], yB[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -387,12 +391,20 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             const int col = 4 * s2 + (l >> 4);
             const float av = wq[(l & 15) * WQS + col];
             const float aq = wq[(GRP + (l & 15)) * WQS + col];
+#ifndef R3DG_EXP_NOXMFMA  // timing experiments only (results invalid): drop the X / Y products
 #pragma unroll
             for (int xb = 0; xb < NXB; ++xb)
                 accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
+#else
+            accX[0][s2 & 3] += av;
+#endif
             const float yo = (float)(s2 >> 1) - 3.5f;
             const float by = yA[s2 & 1] + yo * (yB[s2 & 1] + yo * yC);
+#ifndef R3DG_EXP_NOYMFMA
             accY = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, by, accY, 0, 0, 0);
+#else
+            accY[s2 & 3] += aq * by;
+#endif
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {

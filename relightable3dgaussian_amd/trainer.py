@@ -101,11 +101,20 @@ class GaussianTrainState:
         return st
 
     def widths(self):
-        return [int(np.prod(s)) for _, s in self.groups]
+        # the group layout never changes after construction (densification changes P only):
+        # computed once, so a step's host work stays small beside its ~0.2 ms kernel
+        w = getattr(self, "_widths", None)
+        if w is None:
+            w = self._widths = [int(np.prod(s)) for _, s in self.groups]
+        return w
 
     def roles(self):
-        names = [n for n, _ in self.groups]
-        return [names.index("xyz"), names.index("scaling"), names.index("rotation"), names.index("opacity")]
+        r = getattr(self, "_roles", None)
+        if r is None:
+            names = [n for n, _ in self.groups]
+            r = self._roles = [names.index("xyz"), names.index("scaling"), names.index("rotation"),
+                               names.index("opacity")]
+        return r
 
     def total(self):
         return self.P * sum(self.widths())
