@@ -243,6 +243,30 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
+#ifndef R3DG_BWD_YBF16
+#define R3DG_BWD_YBF16 1  // the moment (Y) products on the bf16 MFMA, q split into three bf16 terms
+#endif
+#ifndef R3DG_BWD_XBF16
+#define R3DG_BWD_XBF16 1  // the colour/feature/depth (X) products on the bf16 MFMA: w in three bf16
+                          // terms, the upstream gradients in two
+#endif
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// x = h + m + o to within 2^-24 |x|: three bf16 terms, each the round-to-nearest of what the
+// previous ones left (the differences are exact in f32), so h*y + m*y + o*y with y exact in bf16
+// (the pixel moments 1, x, y, x^2, xy, y^2 of half-integer offsets are) gives the f32 product.
+__device__ __forceinline__ void split_bf16x3(const float (&x)[8], bf16x8& h, bf16x8& m, bf16x8& o) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const __bf16 hb = (__bf16)x[i];
+        const float r = x[i] - (float)hb;
+        const __bf16 mb = (__bf16)r;
+        h[i] = hb;
+        m[i] = mb;
+        o[i] = (__bf16)(r - (float)mb);
+    }
+}
+
 #ifndef R3DG_BWDG_NB
 #define R3DG_BWDG_NB 64  // instances per staged batch of the DMA-staged kernel
 #endif
@@ -295,7 +319,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     float* wq = reinterpret_cast<float*>(s_lds + w * WQF4);
     int* s_max_last = reinterpret_cast<int*>(stage + 2 * SBUF);
 
+#if !R3DG_BWD_XBF16
     float bX[NXB][16];
+#else
+    // B operand of the X products (16x16x32 layout: lane l holds X[pixel 32b + 8(l >> 4) + i][channel
+    // l & 15]) as two bf16 terms, X = hi + lo to within 2^-17 |X|
+    bf16x8 bXh[NXB][2], bXl[NXB][2];
+#endif
     {
 #pragma unroll
         for (int xb = 0; xb < NXB; ++xb) {
@@ -309,8 +339,20 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 wq[c * WQS + l] = v;
             }
             wave_lds_sync();
+#if !R3DG_BWD_XBF16
 #pragma unroll
             for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
+#else
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float x = wq[(l & 15) * WQS + 32 * b + 8 * (l >> 4) + i];
+                    const __bf16 hb = (__bf16)x;
+                    bXh[xb][b][i] = hb;
+                    bXl[xb][b][i] = (__bf16)(x - (float)hb);
+                }
+#endif
             wave_lds_sync();
         }
     }
@@ -368,12 +410,28 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         u = __builtin_fmaf(ae, diff, u);
     };
 
+#if R3DG_BWD_YBF16
+    // B operand of the moment products, constant: lane l holds Y[pixel 32b + 8(l >> 4) + i][l & 15]
+    // for K-block b (16x16x32 layout), pixel p = (p >> 3) * 8 + (p & 7) about the quadrant centre
+    bf16x8 yb[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int p = 32 * b + 8 * (l >> 4) + i;
+            const float x = (float)(p & 7) - 3.5f, y = (float)(p >> 3) - 3.5f;
+            const float v = nch == 0 ? 1.f : nch == 1 ? x : nch == 2 ? y : nch == 3 ? x * x : nch == 4 ? x * y
+                          : nch == 5 ? y * y : 0.f;
+            yb[b][i] = (__bf16)v;  // exact: at most 6 significant bits
+        }
+#endif
     auto flush = [&](int r) {
         if (l == 0) R3DG_EXP_ADD(1, 1);
 #ifdef R3DG_EXP_NOFLUSH  // timing experiment only (results invalid): no reduction, no rows
         (void)r;
         return;
 #endif
+#if !R3DG_BWD_YBF16
         float yA[2], yB[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -382,6 +440,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             yB[h] = nch == 2 ? 1.f : (nch == 4 ? xo : 0.f);
         }
         const float yC = nch == 5 ? 1.f : 0.f;
+#endif
         wave_lds_sync();
         floatx4 accX[NXB], accY = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -389,8 +448,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
         for (int s2 = 0; s2 < 16; ++s2) {
             const int col = 4 * s2 + (l >> 4);
+#if !R3DG_BWD_XBF16
             const float av = wq[(l & 15) * WQS + col];
+#endif
+#if !R3DG_BWD_YBF16
             const float aq = wq[(GRP + (l & 15)) * WQS + col];
+#endif
+#if !R3DG_BWD_XBF16
 #ifndef R3DG_EXP_NOXMFMA  // timing experiments only (results invalid): drop the X / Y products
 #pragma unroll
             for (int xb = 0; xb < NXB; ++xb)
@@ -398,6 +462,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #else
             accX[0][s2 & 3] += av;
 #endif
+#endif
+#if !R3DG_BWD_YBF16
             const float yo = (float)(s2 >> 1) - 3.5f;
             const float by = yA[s2 & 1] + yo * (yB[s2 & 1] + yo * yC);
 #ifndef R3DG_EXP_NOYMFMA
@@ -405,7 +471,45 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #else
             accY[s2 & 3] += aq * by;
 #endif
+#endif
         }
+#if R3DG_BWD_XBF16
+        // w rows times the upstream gradients on the bf16 MFMA: w = w1 + w2 + w3 (three terms), X =
+        // X1 + X2; the five products above 2^-24 of w X, smallest first
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const float* src = wq + (l & 15) * WQS + 32 * b + 8 * (l >> 4);
+            float wv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wv[i] = src[i];
+            bf16x8 h, m, o;
+            split_bf16x3(wv, h, m, o);
+#pragma unroll
+            for (int xb = 0; xb < NXB; ++xb) {
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o, bXh[xb][b], accX[xb], 0, 0, 0);
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bXl[xb][b], accX[xb], 0, 0, 0);
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bXh[xb][b], accX[xb], 0, 0, 0);
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXl[xb][b], accX[xb], 0, 0, 0);
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
+            }
+        }
+#endif
+#if R3DG_BWD_YBF16
+        // q rows times the moments on the bf16 MFMA (16 cycles per K = 32, against 32 per K = 4 in
+        // f32): three exact-sum bf16 terms of q per K-block
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const float* src = wq + (GRP + (l & 15)) * WQS + 32 * b + 8 * (l >> 4);
+            float qv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) qv[i] = src[i];
+            bf16x8 h, m, o;
+            split_bf16x3(qv, h, m, o);
+            accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, yb[b], accY, 0, 0, 0);
+            accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, yb[b], accY, 0, 0, 0);
+            accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o, yb[b], accY, 0, 0, 0);
+        }
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = (l >> 4) * 4 + i;

@@ -305,7 +305,9 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         // batch `base` has landed (every wave waited for its own DMA) and nobody reads the other
         // buffer any more
         const bool all_done = __syncthreads_count(done) == kBlock;
-        if (base > 0) write_bits(base - NB, NB, buf ^ 1);  // the previous batch's flags
+        // the previous batch's flags, before the DMA issue: folding them after wave 0's DMA issue
+        // measured 0.556 vs 0.480 ms
+        if (base > 0) write_bits(base - NB, NB, buf ^ 1);
         if (all_done) break;
         if (base + NB < n) {  // block-uniform: stage the next batch while this one blends
             issue(gnext, buf ^ 1);
