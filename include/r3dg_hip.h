@@ -123,9 +123,9 @@ size_t r3dg_geom_state_bytes(int P, int S);
 
 /* Debug / parity accessors into the opaque state buffers (tile keys, sort order, ranges). */
 typedef struct r3dg_binning_view {
-    const uint32_t* tile_sorted;  /* [L] tile of each sorted instance; the reference's sort key is
-                                     tile<<32 | depth bits of point_list[i], ascending */
-    const uint32_t* point_list;   /* [L] Gaussian ids in sorted order (reference point_list) */
+    const uint32_t* point_list;   /* [L] Gaussian ids in sorted order (reference point_list); the
+                                     reference's sort key of position i is tile << 32 | depth bits
+                                     of point_list[i], with the tile given by ranges */
     const uint32_t* ranges;       /* [tiles,2] from the image buffer */
     const uint32_t* point_offsets;/* [P] inclusive scan of tiles touched */
     const float* depths;          /* [P] */

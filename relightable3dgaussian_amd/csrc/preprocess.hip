@@ -167,6 +167,9 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     const int ng = min(256, a.P - g0);
     const int M3 = 3 * a.M;
     const bool use_sh = a.sh && !a.colors_precomp;
+    // the per-tile counters of the atomic binning (bin_atomic_kernel) start at zero
+    if (a.tile_count)
+        for (int i = idx; i < a.num_tiles; i += (int)(gridDim.x * 256)) a.tile_count[i] = 0u;
     if (use_sh) {
         const float* src = a.sh + (size_t)g0 * M3;
         for (int f = t; f < ng * M3; f += 256) {
@@ -213,136 +216,354 @@ __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* _
     present[idx] = xform_point4x3(p, view).z <= 0.2f ? 0 : 1;
 }
 
-// duplicateWithKeys (rasterizer_impl.cu:72-113). Block b expands the Gaussians [256b, 256b+256)
-// into their tiles, row-major over each rect as the reference, at their Gaussian-major slots
-// offsets[g-1] + k: the block's instances are one contiguous slot range, written cooperatively
-// (coalesced; output position q finds its Gaussian by binary search over the block's instance
-// offsets). The key is the tile alone: a stable sort by tile keeps each tile's instances in
-// ascending Gaussian order, and tile_depth_sort_kernel then orders every tile by depth, stably --
-// together the reference's stable sort by (tile << 32 | depth bits) over the Gaussian-major list.
-// The four backward row flags of each slot (render_bwd.hip) are zeroed on the way.
-__global__ void __launch_bounds__(256) duplicate_kernel(int P, const uint32_t* __restrict__ offsets,
-                                                        const float2* __restrict__ means2D,
-                                                        const int* __restrict__ radii, int grid_x, int grid_y,
-                                                        uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ gid_out,
-                                                        uint32_t* __restrict__ flags, float4* __restrict__ records,
-                                                        int rec4) {
-    __shared__ uint32_t s_end[256];  // inclusive end of each Gaussian's instances, block-relative
-    __shared__ int s_x0[256], s_y0[256], s_w[256];
-    const int t = threadIdx.x;
-    const int i0 = blockIdx.x * 256;
-    const int n = min(256, P - i0);
-    const uint32_t base = i0 == 0 ? 0u : offsets[i0 - 1];
-    if (t < n) {
-        const int g = i0 + t;
-        s_end[t] = offsets[g] - base;
-        const int r = radii[g];
+// Binning: duplicateWithKeys + SortPairs + identifyTileRanges (rasterizer_impl.cu:72-140, 343-383).
+// The reference writes one (tile << 32 | depth) key per instance in Gaussian-major slot order and
+// radix-sorts all L of them (45 bits, stable). Its result is every tile's instances ordered by
+// (depth bits, Gaussian id): a stable sort of a Gaussian-major list breaks depth ties by Gaussian.
+// Here the tile grouping is a counting sort with no order inside a tile, and
+// tile_depth_sort_kernel then orders every tile by (depth bits, Gaussian id):
+//   1. bin_count_kernel: workgroup b (one per CU) counts the instances of its Gaussian range per
+//      tile with LDS counters and writes its row hist[b, :];
+//   2. bin_totals_kernel: per-tile totals (column sums of hist);
+//   3. tile_ranges_kernel: exclusive scan of the totals -> ranges (the reference's (0, 0) for
+//      empty tiles), each tile's first position, and the longest-first tile order;
+//   4. bin_offsets_kernel: hist[b, t] = first position of workgroup b's instances of tile t;
+//   5. bin_scatter_kernel: every instance takes the next position of its (workgroup, tile) from
+//      an LDS counter and writes (depth bits, Gaussian id) there -- one 8-byte store, and the
+//      depth sort reads its keys coalesced instead of gathering them per instance (also zeroes
+//      the backward's row flags and stores each Gaussian's first slot in its render record).
+// No global atomics: they execute at the memory side (MI355X_MICROARCH.md "Global float
+// atomics"), one 64-B request per scattered lane -- a first version with one per instance took
+// 0.18 ms per pass at M1. Steps 1-4 need only the scan of tiles touched, so they run while the
+// host reads num_rendered back and allocates the binning state. Workgroups enumerate their
+// instances load-balanced, kBinSub Gaussians at a time: slot q finds its Gaussian by binary search
+// over the staged instance offsets, and its tile is the row-major index of q - the Gaussian's first
+// slot in its rect (duplicateWithKeys' order). Above kBinMaxTiles tiles the LDS counters do not
+// fit and bin_atomic_kernel takes one global atomic per instance instead (same result).
+
+// The instances of Gaussians [g0, g0 + n), n <= kBinSub, staged in LDS: visit(tile, g, key) once per
+// instance (key: the Gaussian's depth bits, scatter passes only). Every thread takes a contiguous run of the range's slots: one binary search for the
+// run's first Gaussian, then the rect walked row-major (duplicateWithKeys' order) -- the search's
+// dependent LDS reads are paid once per run, not once per instance. Scatter passes also zero the
+// backward's row flags of the range's slots (coalesced) and store each Gaussian's first slot.
+template <class Visit>
+__device__ __forceinline__ void bin_enumerate(const BinArgs& a, int g0, int n, uint32_t* s_end, int* s_x0, int* s_y0,
+                                              int* s_w, bool scatter, Visit visit) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    const uint32_t base = g0 == 0 ? 0u : a.offsets[g0 - 1];
+    __syncthreads();  // the previous range's enumeration is done with the staging arrays
+    for (int i = t; i < n; i += nt) {
+        const int g = g0 + i;
+        s_end[i] = a.offsets[g] - base;
+        const int r = a.radii[g];
         int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
         if (r > 0) {
-            const float2 m = means2D[g];
-            get_rect(m.x, m.y, r, grid_x, grid_y, x0, y0, x1, y1);
-            if (records)  // the Gaussian's first slot, for the backward's rows
-                reinterpret_cast<float*>(records + (size_t)g * rec4 + 1)[2] =
-                    __uint_as_float(g == 0 ? 0u : offsets[g - 1]);
+            const float2 m = a.means2D[g];
+            get_rect(m.x, m.y, r, a.grid_x, a.grid_y, x0, y0, x1, y1);
+            if (scatter && a.records)
+                reinterpret_cast<float*>(a.records + (size_t)g * a.rec4 + 1)[2] =
+                    __uint_as_float(g == 0 ? 0u : a.offsets[g - 1]);
         }
-        s_x0[t] = x0;
-        s_y0[t] = y0;
-        s_w[t] = max(x1 - x0, 1);
+        s_x0[i] = x0;
+        s_y0[i] = y0;
+        s_w[i] = max(x1 - x0, 1);
     }
     __syncthreads();
     const uint32_t total = s_end[n - 1];
-    for (uint32_t q = t; q < total; q += 256) {
-        int lo = 0, hi = n - 1;  // first Gaussian whose end > q
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_end[mid] > q) hi = mid;
-            else lo = mid + 1;
+    if (scatter && a.flags)
+        for (uint32_t q = t; q < total; q += nt) a.flags[base + q] = 0u;
+    const uint32_t per = (total + nt - 1) / nt;
+    uint32_t q = min((uint32_t)t * per, total);
+    const uint32_t q1 = min(q + per, total);
+    if (q >= q1) return;
+    int lo = 0, hi = n - 1;  // first Gaussian whose end > q
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_end[mid] > q) hi = mid;
+        else lo = mid + 1;
+    }
+    uint32_t end = s_end[lo];
+    const uint32_t k = q - (lo == 0 ? 0u : s_end[lo - 1]);
+    int w = s_w[lo], x0 = s_x0[lo];
+    int x = x0 + (int)(k % (uint32_t)w), y = s_y0[lo] + (int)(k / (uint32_t)w);
+    uint32_t key = scatter ? a.depth_keys[g0 + lo] : 0u;
+    for (;;) {
+        visit((uint32_t)(y * a.grid_x + x), (uint32_t)(g0 + lo), key);
+        if (++q >= q1) break;
+        if (q < end) {
+            if (++x == x0 + w) { x = x0; ++y; }
+        } else {  // next Gaussian with instances
+            do { ++lo; } while (s_end[lo] <= q);
+            end = s_end[lo];
+            w = s_w[lo]; x0 = s_x0[lo]; x = x0; y = s_y0[lo];
+            if (scatter) key = a.depth_keys[g0 + lo];
         }
-        const uint32_t k = q - (lo == 0 ? 0u : s_end[lo - 1]);
-        const int w = s_w[lo];
-        const int x = s_x0[lo] + (int)(k % (uint32_t)w), y = s_y0[lo] + (int)(k / (uint32_t)w);
-        tile_keys[base + q] = (uint32_t)(y * grid_x + x);
-        gid_out[base + q] = (uint32_t)(i0 + lo);
-        if (flags) flags[base + q] = 0u;
     }
 }
 
-// identifyTileRanges (rasterizer_impl.cu:118-140) as one binary search per tile over the sorted
-// tile ids: every tile's range is written (empty tiles (0, 0), the reference's memset value), so no
-// memset is needed.
-__global__ void __launch_bounds__(256) tile_ranges_kernel(int T, int L, const uint32_t* __restrict__ tiles,
-                                                          uint2* __restrict__ ranges) {
-    const int tile = blockIdx.x * blockDim.x + threadIdx.x;
-    if (tile >= T) return;
-    auto lower = [&](uint32_t key) {
-        int lo = 0, hi = L;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (tiles[mid] < key) lo = mid + 1;
-            else hi = mid;
-        }
-        return (uint32_t)lo;
-    };
-    const uint32_t b = lower((uint32_t)tile), e = lower((uint32_t)tile + 1u);
-    ranges[tile] = b < e ? make_uint2(b, e) : make_uint2(0u, 0u);  // empty: (0, 0) as the reference's memset
+// Gaussian range of binning workgroup b: whole kBinSub sub-ranges, split evenly
+__device__ __forceinline__ void bin_range(const BinArgs& a, int& g_begin, int& g_end) {
+    const int nsub = (a.P + kBinSub - 1) / kBinSub;
+    const int b = blockIdx.x;
+    g_begin = (int)((long long)b * nsub / a.nblk) * kBinSub;
+    g_end = min((int)((long long)(b + 1) * nsub / a.nblk) * kBinSub, a.P);
 }
 
-// Backward (and depth-sort) launch order, longest tiles first: one workgroup bucket-sorts the
-// tiles by instance count (bucket = count / 4, capped; descending). Only the schedule depends on
-// this order, so the order within a bucket, which LDS atomics leave unspecified, changes no result.
-__global__ void __launch_bounds__(1024) tile_order_kernel(int T, const uint2* __restrict__ ranges,
-                                                          uint32_t* __restrict__ order) {
+__global__ void __launch_bounds__(kBinThreads) bin_count_kernel(BinArgs a) {
+    extern __shared__ uint32_t s_dyn[];
+    uint32_t* s_cnt = s_dyn;  // [T]
+    uint32_t* s_end = s_dyn + a.T;
+    int* s_x0 = reinterpret_cast<int*>(s_end + kBinSub);
+    int* s_y0 = s_x0 + kBinSub;
+    int* s_w = s_y0 + kBinSub;
+    for (int i = threadIdx.x; i < a.T; i += kBinThreads) s_cnt[i] = 0u;
+    int gb, ge;
+    bin_range(a, gb, ge);
+    for (int g0 = gb; g0 < ge; g0 += kBinSub)
+        bin_enumerate(a, g0, min(kBinSub, ge - g0), s_end, s_x0, s_y0, s_w, false,
+                      [&](uint32_t tile, uint32_t, uint32_t) { atomicAdd(s_cnt + tile, 1u); });
+    __syncthreads();
+    uint32_t* row = a.hist + (size_t)blockIdx.x * a.T;
+    for (int i = threadIdx.x; i < a.T; i += kBinThreads) row[i] = s_cnt[i];
+}
+
+// tile_work[t] = sum over workgroups of hist[b, t]: 64 tiles per workgroup (one per lane), wave w
+// of 16 sums rows w, w + 16, ... (16 independent loads in flight per wave for 256 rows)
+__global__ void __launch_bounds__(1024) bin_totals_kernel(BinArgs a) {
+    __shared__ uint32_t s_part[16][64];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int tile = blockIdx.x * 64 + l;
+    uint32_t s = 0;
+    if (tile < a.T)
+        for (int b = w; b < a.nblk; b += 16) s += a.hist[(size_t)b * a.T + tile];
+    s_part[w][l] = s;
+    __syncthreads();
+    if (w == 0 && tile < a.T) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) tot += s_part[k][l];
+        a.tile_work[tile] = tot;
+    }
+}
+
+// hist[b, t] = tile_work[t] (the tile's first position) + sum of hist[b', t] for b' < b: 64 tiles
+// per workgroup, wave w of 16 owns the contiguous rows [w nblk / 16, (w + 1) nblk / 16)
+__global__ void __launch_bounds__(1024) bin_offsets_kernel(BinArgs a) {
+    __shared__ uint32_t s_part[16][64];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int tile = blockIdx.x * 64 + l;
+    const int r0 = w * a.nblk / 16, r1 = (w + 1) * a.nblk / 16;
+    uint32_t s = 0;
+    if (tile < a.T)
+        for (int b = r0; b < r1; ++b) s += a.hist[(size_t)b * a.T + tile];
+    s_part[w][l] = s;
+    __syncthreads();
+    if (tile >= a.T) return;
+    uint32_t run = a.tile_work[tile];
+    for (int k = 0; k < w; ++k) run += s_part[k][l];
+    for (int b = r0; b < r1; ++b) {
+        uint32_t* h = a.hist + (size_t)b * a.T + tile;
+        const uint32_t c = *h;
+        *h = run;
+        run += c;
+    }
+}
+
+__global__ void __launch_bounds__(kBinThreads) bin_scatter_kernel(BinArgs a) {
+    extern __shared__ uint32_t s_dyn[];
+    uint32_t* s_pos = s_dyn;  // [T] next position of this workgroup's instances of each tile
+    uint32_t* s_end = s_dyn + a.T;
+    int* s_x0 = reinterpret_cast<int*>(s_end + kBinSub);
+    int* s_y0 = s_x0 + kBinSub;
+    int* s_w = s_y0 + kBinSub;
+    const uint32_t* row = a.hist + (size_t)blockIdx.x * a.T;
+    for (int i = threadIdx.x; i < a.T; i += kBinThreads) s_pos[i] = row[i];
+    int gb, ge;
+    bin_range(a, gb, ge);
+    for (int g0 = gb; g0 < ge; g0 += kBinSub)
+        bin_enumerate(a, g0, min(kBinSub, ge - g0), s_end, s_x0, s_y0, s_w, true,
+                      [&](uint32_t tile, uint32_t g, uint32_t key) {
+                          a.pairs[atomicAdd(s_pos + tile, 1u)] = make_uint2(key, g);
+                      });
+}
+
+// Fallback above kBinMaxTiles tiles: one global atomic per instance on the per-tile counters
+// (counting pass; preprocess zeroed them) or cursors (scatter pass).
+template <bool SCATTER>
+__global__ void __launch_bounds__(256) bin_atomic_kernel(BinArgs a) {
+    __shared__ uint32_t s_end[256];
+    __shared__ int s_x0[256], s_y0[256], s_w[256];
+    const int g0 = blockIdx.x * 256;
+    bin_enumerate(a, g0, min(256, a.P - g0), s_end, s_x0, s_y0, s_w, SCATTER,
+                  [&](uint32_t tile, uint32_t g, uint32_t key) {
+                      if constexpr (SCATTER) a.pairs[atomicAdd(a.tile_work + tile, 1u)] = make_uint2(key, g);
+                      else atomicAdd(a.tile_work + tile, 1u);
+                  });
+}
+
+static size_t bin_lds_bytes(int T) { return sizeof(uint32_t) * ((size_t)T + 4 * kBinSub); }
+
+// dynamic LDS above 64 KiB must be allowed per kernel (T > 12288 tiles, e.g. 4K frames)
+template <class K>
+static hipError_t allow_lds(K kernel, size_t bytes) {
+    if (bytes <= 65536) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes);
+}
+
+// Exclusive scan of one value per thread over a 1024-thread block: wave scans by lane shuffles,
+// then the 16 wave totals (two barriers).
+__device__ __forceinline__ uint32_t block_exclusive_scan_1024(uint32_t v, uint32_t* s_wave) {
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (l >= o) x += y;
+    }
+    if (l == 63) s_wave[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int k = 0; k < w; ++k) pre += s_wave[k];
+    __syncthreads();  // s_wave may be reused
+    return pre + x - v;
+}
+
+// identifyTileRanges (rasterizer_impl.cu:118-140) from the per-tile counts: one workgroup scans
+// them (tile t's range starts after every lower tile's instances, as in the sorted list), writes
+// every tile's range (empty tiles (0, 0), the reference's memset value) and turns the counts into
+// the tiles' first positions. Then the backward / depth-sort launch order, longest tiles first: a
+// bucket sort by instance count (bucket = count / 4, capped; descending). Only the schedule depends
+// on the order, so the order within a bucket, which LDS atomics leave unspecified, changes no result
+// (measured: exact-count buckets, which scatter the tiles of a bucket spatially, slowed the
+// backward by 3 %). Thread t owns the PER tiles [t PER, t PER + PER), held in registers: one round of
+// independent loads (PER = 0: any T, counts re-read).
+template <int PER>
+__global__ void __launch_bounds__(1024) tile_ranges_kernel(int T, uint32_t* __restrict__ work,
+                                                           uint2* __restrict__ ranges, uint32_t* __restrict__ order) {
     constexpr int NBK = 1024;
     __shared__ uint32_t hist[NBK];
-    __shared__ uint32_t scan[2][NBK];
+    __shared__ uint32_t s_wave[16];
     const int t = threadIdx.x;
+    const int per = PER > 0 ? PER : (T + 1023) / 1024;
+    const int b0 = min(t * per, T), b1 = min(b0 + per, T);
+    auto bucket = [](uint32_t c) { return (int)min(c >> 2, (uint32_t)(NBK - 1)); };
     hist[t] = 0;
-    __syncthreads();
-    auto bucket = [&](int tile) {
-        const uint2 r = ranges[tile];
-        return (int)min((r.y - r.x) >> 2, (uint32_t)(NBK - 1));
-    };
-    for (int i = t; i < T; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
-    __syncthreads();
-    // exclusive scan in descending bucket order (Hillis-Steele over the reversed histogram)
-    const uint32_t v = hist[NBK - 1 - t];
-    int cur = 0;
-    scan[0][t] = v;
-    __syncthreads();
-    for (int o = 1; o < NBK; o <<= 1) {
-        const uint32_t x = scan[cur][t] + (t >= o ? scan[cur][t - o] : 0u);
-        scan[cur ^ 1][t] = x;
-        cur ^= 1;
-        __syncthreads();
+    uint32_t c[PER > 0 ? PER : 1];
+    uint32_t sum = 0;
+    if constexpr (PER > 0) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) c[k] = b0 + k < b1 ? work[b0 + k] : 0u;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) sum += c[k];
+    } else {
+        for (int i = b0; i < b1; ++i) sum += work[i];
     }
-    hist[NBK - 1 - t] = scan[cur][t] - v;  // now the cursor of bucket NBK-1-t
+    uint32_t run = block_exclusive_scan_1024(sum, s_wave);
+    if constexpr (PER > 0) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = b0 + k;
+            if (i < b1) {
+                ranges[i] = c[k] ? make_uint2(run, run + c[k]) : make_uint2(0u, 0u);
+                work[i] = run;
+                run += c[k];
+                if (order) atomicAdd(&hist[bucket(c[k])], 1u);
+            }
+        }
+    } else {
+        for (int i = b0; i < b1; ++i) {
+            const uint32_t ci = work[i];
+            ranges[i] = ci ? make_uint2(run, run + ci) : make_uint2(0u, 0u);
+            work[i] = run;
+            run += ci;
+            if (order) atomicAdd(&hist[bucket(ci)], 1u);
+        }
+    }
+    if (!order) return;  // block-uniform
     __syncthreads();
-    for (int i = t; i < T; i += 1024) order[atomicAdd(&hist[bucket(i)], 1u)] = (uint32_t)i;
+    // exclusive scan in descending bucket order (over the reversed histogram)
+    const uint32_t v = hist[NBK - 1 - t];
+    const uint32_t ex = block_exclusive_scan_1024(v, s_wave);
+    hist[NBK - 1 - t] = ex;  // now the cursor of bucket NBK-1-t
+    __syncthreads();
+    if constexpr (PER > 0) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+            if (b0 + k < b1) order[atomicAdd(&hist[bucket(c[k])], 1u)] = (uint32_t)(b0 + k);
+    } else {
+        for (int i = b0; i < b1; ++i) {
+            const uint2 r = ranges[i];
+            order[atomicAdd(&hist[bucket(r.y - r.x)], 1u)] = (uint32_t)i;
+        }
+    }
 }
 
-// The depth half of the reference's (tile << 32 | depth bits) sort: every tile's instances,
-// ascending Gaussian ids after the stable tile sort, sorted stably by the Gaussians' depth bits
-// (the reference's order: depth, ties by Gaussian id). One workgroup per tile, longest tiles
-// first. A chunk of the tile is sorted in registers / LDS (rocPRIM block radix sort, 4 passes of
-// 8 bits) -- 1024-instance chunks for tiles of up to 1024 instances, 2048-instance chunks for
-// longer ones (both sorters share one LDS union: 16 KB, still 8 waves/SIMD); a tile longer than
-// one chunk sorts each chunk into a run and merges run pairs (stable merge path) through the
-// scratch buffers, ping-pong, landing in point_list.
+hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st) {
+    if (a.T <= 0) return hipSuccess;
+    if (a.P > 0) {
+        if (a.hist) {
+            const hipError_t e = allow_lds(bin_count_kernel, bin_lds_bytes(a.T));
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(bin_count_kernel, dim3(a.nblk), dim3(kBinThreads), bin_lds_bytes(a.T), st, a);
+            hipLaunchKernelGGL(bin_totals_kernel, dim3((a.T + 63) / 64), dim3(1024), 0, st, a);
+        } else {
+            hipLaunchKernelGGL(bin_atomic_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
+        }
+    }
+    if (a.T <= 8 * 1024)
+        hipLaunchKernelGGL(tile_ranges_kernel<8>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
+    else if (a.T <= 40 * 1024)
+        hipLaunchKernelGGL(tile_ranges_kernel<40>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
+    else
+        hipLaunchKernelGGL(tile_ranges_kernel<0>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
+    if (a.P > 0 && a.hist) hipLaunchKernelGGL(bin_offsets_kernel, dim3((a.T + 63) / 64), dim3(1024), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_scatter(const BinArgs& a, hipStream_t st) {
+    if (a.P <= 0 || a.T <= 0) return hipSuccess;
+    if (a.hist) {
+        const hipError_t e = allow_lds(bin_scatter_kernel, bin_lds_bytes(a.T));
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(bin_scatter_kernel, dim3(a.nblk), dim3(kBinThreads), bin_lds_bytes(a.T), st, a);
+    } else {
+        hipLaunchKernelGGL(bin_atomic_kernel<true>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
+    }
+    return hipGetLastError();
+}
+
+// The depth half of the binning: every tile's instances, in whatever order the scatter left them,
+// sorted by (depth bits, Gaussian id) -- the reference's stable (tile << 32 | depth) sort of the
+// Gaussian-major list orders a tile by depth and breaks ties by Gaussian id. One workgroup per tile,
+// longest tiles first. A chunk of the tile is sorted in registers / LDS (rocPRIM block radix sort,
+// 4 passes of 8 bits) -- 1024-instance chunks for tiles of up to 1024 instances, 2048-instance
+// chunks for longer ones (both sorters share one LDS union: 16 KB, still 8 waves/SIMD). A chunk
+// with equal depth bits (cloned Gaussians share a depth until they move) is sorted again: by
+// Gaussian id, then stably by depth. A tile longer than one chunk sorts each chunk into a run and
+// merges run pairs (merge path, (depth, id) compared lexicographically) through the scratch
+// buffers, ping-pong, landing in point_list.
 constexpr int kSortBT = 256;
 using TileDepthSort4 = rocprim::block_radix_sort<uint32_t, kSortBT, 4, uint32_t>;
 using TileDepthSortL = rocprim::block_radix_sort<uint32_t, kSortBT, R3DG_SORT_LONG_IPT, uint32_t>;
 union TileDepthSortStorage {
     typename TileDepthSort4::storage_type s4;
     typename TileDepthSortL::storage_type sl;
+    uint32_t keys[kSortBT * R3DG_SORT_LONG_IPT];  // the sorted chunk's keys (tie test)
 };
 
 __device__ __forceinline__ uint32_t nt_load(const uint32_t* p) { return __builtin_nontemporal_load(p); }
 
+// (depth bits, Gaussian id) order; Gaussian ids are unique within a tile
+__device__ __forceinline__ bool kv_less(uint32_t ka, uint32_t va, uint32_t kb, uint32_t vb) {
+    return ka < kb || (ka == kb && va < vb);
+}
+
 // chunks of kSortBT * IPT instances of the tile [s, s + n) sorted into runs at (rk, rv)
 template <int IPT, class Sort, class Storage>
-__device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_t nchunks, const uint32_t* depth_keys,
-                                                 const uint32_t* point_list, uint32_t* rk, uint32_t* rv,
-                                                 Storage& storage) {
+__device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_t nchunks, const uint2* pairs,
+                                                 uint32_t* rk, uint32_t* rv,
+                                                 TileDepthSortStorage& st, Storage& storage) {
     constexpr uint32_t kChunk = kSortBT * IPT;
     const int t = threadIdx.x;
     for (uint32_t c = 0; c < nchunks; ++c) {
@@ -351,12 +572,29 @@ __device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {  // blocked arrangement: item index = t * IPT + k
             const uint32_t i = c0 + (uint32_t)(t * IPT + k);
-            const uint32_t g = i < n ? point_list[s + i] : 0xffffffffu;
-            vals[k] = g;
-            keys[k] = i < n ? depth_keys[g] : 0xffffffffu;  // visible depths < 0x7f800000: pads sort last
+            // visible depths < 0x7f800000: pads sort last
+            const uint2 kv = i < n ? pairs[s + i] : make_uint2(0xffffffffu, 0xffffffffu);
+            keys[k] = kv.x;
+            vals[k] = kv.y;
         }
         if (c > 0) __syncthreads();  // storage reuse
         Sort().sort(keys, vals, storage, 0, 32);
+        // equal depth bits anywhere in the chunk (pads excluded: they are the all-ones key)?
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) st.keys[t * IPT + k] = keys[k];
+        __syncthreads();
+        bool tie = false;
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const int i = t * IPT + k;
+            if (i + 1 < (int)kChunk && keys[k] != 0xffffffffu && st.keys[i + 1] == keys[k]) tie = true;
+        }
+        if (__syncthreads_or(tie)) {  // block-uniform: id order first, then stably by depth
+            Sort().sort(vals, keys, storage, 0, 32);
+            __syncthreads();
+            Sort().sort(keys, vals, storage, 0, 32);
+        }
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const uint32_t i = c0 + (uint32_t)(t * IPT + k);
@@ -368,19 +606,21 @@ __device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_
     }
 }
 
-__global__ void __launch_bounds__(kSortBT) __attribute__((amdgpu_waves_per_eu(8))) tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges,
-                                                                  const uint32_t* __restrict__ order,
-                                                                  const uint32_t* __restrict__ depth_keys,
-                                                                  uint32_t* __restrict__ point_list, uint32_t* kA,
-                                                                  uint32_t* vA, uint32_t* kB) {
+__global__ void __launch_bounds__(kSortBT) __attribute__((amdgpu_waves_per_eu(8)))
+tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges, const uint32_t* __restrict__ order,
+                       const uint2* __restrict__ pairs, uint32_t* __restrict__ point_list,
+                       uint32_t* kA, uint32_t* vA, uint32_t* kB) {
     __shared__ TileDepthSortStorage storage;
     const int b = blockIdx.x;
     if (b >= T) return;
     const int tile = order ? (int)order[b] : b;
     const uint2 rg = ranges[tile];
     const uint32_t s = rg.x, n = rg.y - rg.x;
-    if (n <= 1) return;
     const int t = threadIdx.x;
+    if (n <= 1) {
+        if (n == 1 && t == 0) point_list[s] = pairs[s].y;
+        return;
+    }
     // sorter capacity by tile length (block-uniform); a 2-item sorter for tiles of up to 512
     // instances measured no faster (M1: 0.086 vs 0.083 ms, it spills one VGPR)
     const uint32_t kChunk = n <= kSortBT * 4 ? kSortBT * 4 : kSortBT * R3DG_SORT_LONG_IPT;
@@ -390,8 +630,11 @@ __global__ void __launch_bounds__(kSortBT) __attribute__((amdgpu_waves_per_eu(8)
     // runs go where an even number of merge rounds leaves the result in (kB, point_list)
     uint32_t* rk = (rounds & 1) ? kA : kB;
     uint32_t* rv = (rounds & 1) ? vA : point_list;
-    if (kChunk == kSortBT * 4) sort_tile_chunks<4, TileDepthSort4>(s, n, nchunks, depth_keys, point_list, rk, rv, storage.s4);
-    else sort_tile_chunks<R3DG_SORT_LONG_IPT, TileDepthSortL>(s, n, nchunks, depth_keys, point_list, rk, rv, storage.sl);
+    if (kChunk == kSortBT * 4)
+        sort_tile_chunks<4, TileDepthSort4>(s, n, nchunks, pairs, rk, rv, storage, storage.s4);
+    else
+        sort_tile_chunks<R3DG_SORT_LONG_IPT, TileDepthSortL>(s, n, nchunks, pairs, rk, rv, storage,
+                                                             storage.sl);
     if (nchunks == 1) return;
     __syncthreads();
     uint32_t *sk = rk, *sv = rv, *dk = (rk == kA) ? kB : kA, *dv = (rk == kA) ? point_list : vA;
@@ -404,27 +647,31 @@ __global__ void __launch_bounds__(kSortBT) __attribute__((amdgpu_waves_per_eu(8)
             if (d0 >= d1) continue;
             const uint32_t* A = sk + s + a0;
             const uint32_t* B = sk + s + a1;
-            // merge path: i = number of A items among the first d0 outputs (ties: A first)
+            const uint32_t* Av = sv + s + a0;
+            const uint32_t* Bv = sv + s + a1;
+            // merge path: i = number of A items among the first d0 outputs
             uint32_t lo = d0 > lb ? d0 - lb : 0u, hi = min(d0, la);
             while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (nt_load(A + mid) <= nt_load(B + (d0 - 1 - mid))) lo = mid + 1;
+                const uint32_t mid = (lo + hi) >> 1, o = d0 - 1 - mid;
+                if (!kv_less(nt_load(B + o), nt_load(Bv + o), nt_load(A + mid), nt_load(Av + mid))) lo = mid + 1;
                 else hi = mid;
             }
             uint32_t i = lo, j = d0 - lo;
-            uint32_t ka = i < la ? nt_load(A + i) : 0xffffffffu, kb = j < lb ? nt_load(B + j) : 0xffffffffu;
+            uint32_t ka = 0xffffffffu, va = 0xffffffffu, kb = 0xffffffffu, vb = 0xffffffffu;
+            if (i < la) { ka = nt_load(A + i); va = nt_load(Av + i); }
+            if (j < lb) { kb = nt_load(B + j); vb = nt_load(Bv + j); }
             for (uint32_t d = d0; d < d1; ++d) {
-                const bool takeA = j >= lb || (i < la && ka <= kb);
+                const bool takeA = j >= lb || (i < la && kv_less(ka, va, kb, vb));
                 if (takeA) {
                     dk[s + a0 + d] = ka;
-                    dv[s + a0 + d] = nt_load(sv + s + a0 + i);
+                    dv[s + a0 + d] = va;
                     ++i;
-                    ka = i < la ? nt_load(A + i) : 0xffffffffu;
+                    if (i < la) { ka = nt_load(A + i); va = nt_load(Av + i); }
                 } else {
                     dk[s + a0 + d] = kb;
-                    dv[s + a0 + d] = nt_load(sv + s + a1 + j);
+                    dv[s + a0 + d] = vb;
                     ++j;
-                    kb = j < lb ? nt_load(B + j) : 0xffffffffu;
+                    if (j < lb) { kb = nt_load(B + j); vb = nt_load(Bv + j); }
                 }
             }
         }
@@ -434,9 +681,11 @@ __global__ void __launch_bounds__(kSortBT) __attribute__((amdgpu_waves_per_eu(8)
     }
 }
 
-hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint32_t* depth_keys,
-                                  uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB, hipStream_t st) {
-    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(T), dim3(kSortBT), 0, st, T, ranges, order, depth_keys, point_list,
+hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint2* pairs,
+                                  uint32_t* point_list, uint32_t* kA, uint32_t* vA,
+                                  uint32_t* kB, hipStream_t st) {
+    if (T <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(T), dim3(kSortBT), 0, st, T, ranges, order, pairs, point_list,
                        kA, vA, kB);
     return hipGetLastError();
 }

@@ -65,24 +65,24 @@ struct GeomState {
 };
 
 struct BinningState {
-    // Instances are generated in the reference's Gaussian-major slot order, stably sorted by tile,
-    // then each tile stably by depth bits: the reference's stable sort by (tile << 32 | depth
-    // bits). The sort values are Gaussian ids, so the sorted values are the reference's point_list.
-    uint32_t* tile_keys;    // [L] tile of each instance, slot order (sort input; then depth-sort scratch)
-    uint32_t* tile_sorted;  // [L] tile of each sorted instance
-    uint32_t* gid_in;       // [L] Gaussian of each instance, slot order (sort values; then scratch)
+    // Instances grouped by tile with per-tile counters, then every tile sorted by (depth bits,
+    // Gaussian id): the reference's stable sort by (tile << 32 | depth bits) of its Gaussian-major
+    // instance list (preprocess.hip bin_count_kernel / tile_depth_sort_kernel).
     uint32_t* point_list;   // [L] Gaussian ids in sorted order (reference point_list)
-    uint32_t* keys2;        // [L] depth-sort scratch (tiles longer than one sort chunk)
+    uint2* pairs;           // [L] (depth bits, Gaussian) grouped by tile, unsorted within a tile
+    uint32_t* sort_k1;      // [L] depth-sort scratch (tiles longer than one sort chunk)
+    uint32_t* sort_v1;      // [L]
+    uint32_t* sort_k2;      // [L]
     uint32_t* flags;        // [L] backward row flags, one byte per (slot, quadrant) (render_bwd.hip)
     uint8_t* contrib;       // [L] per sorted position: bit q = a pixel of quadrant q blended it (forward)
-    void* sort_temp;
-    size_t sort_temp_bytes;
 };
 struct ImageState {
     float* final_T;     // [H*W]
     uint32_t* n_contrib;// [H*W]
     uint2* ranges;      // [tiles]
     uint32_t* tile_order;        // [tiles] tiles by descending instance count (blend launch order)
+    uint32_t* tile_work;         // [tiles] binning: instance count per tile, then its first position
+    uint32_t* bin_hist;          // [bin_blocks_max(tiles), tiles] binning: per-workgroup counts / positions
 };
 
 size_t geom_state_bytes(size_t P, int S);

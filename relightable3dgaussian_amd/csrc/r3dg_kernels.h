@@ -4,6 +4,8 @@
 
 #include <hip/hip_ext.h>
 
+#include <algorithm>
+
 #include "r3dg_common.h"
 
 namespace r3dg {
@@ -34,7 +36,32 @@ struct PreprocessArgs {
     float* rgb;
     uint8_t* clamped;
     unsigned int* error_flag;
+    uint32_t* tile_count;  // [num_tiles] zeroed here for the atomic binning (bin_atomic_kernel), or null
+    int num_tiles;
 };
+
+// Binning (duplicateWithKeys + SortPairs + identifyTileRanges, rasterizer_impl.cu:72-140, 343-383)
+// as two passes over the instances with per-tile counters instead of a radix sort over L keys:
+// see preprocess.hip bin_count_kernel.
+struct BinArgs {
+    int P, grid_x, grid_y, rec4, T;
+    int nblk;                 // binning workgroups (bin_blocks); each owns a contiguous Gaussian range
+    const uint32_t* offsets;  // inclusive scan of tiles touched
+    const float2* means2D;
+    const int* radii;
+    uint32_t* tile_work;      // [T] instance count per tile, then the tile's first position
+    uint32_t* hist;           // [nblk, T] per-workgroup tile counts, then positions; null: T too large
+                              // for the LDS counters, every instance takes a global atomic instead
+    const uint32_t* depth_keys;  // [P] float bits of each Gaussian's view depth
+    uint2* pairs;             // [L] scatter pass: (depth bits, Gaussian) of each instance, grouped by tile
+    uint32_t* flags;          // [L] scatter pass: backward row flags of each slot, zeroed
+    float4* records;          // scatter pass: each visible Gaussian's first slot (render record)
+};
+constexpr int kBinThreads = 1024;                  // binning workgroup (one per CU)
+constexpr int kBinSub = 1024;                      // Gaussians staged in LDS at a time
+constexpr int kBinMaxTiles = (163840 - 16 * kBinSub) / 4;  // LDS counters per workgroup (160 KiB)
+// binning workgroups for T tiles: the [nblk, T] count matrix stays <= 8 MiB
+inline int bin_blocks_max(int T) { return T > kBinMaxTiles ? 0 : std::max(1, std::min(256, (1 << 21) / std::max(T, 1))); }
 
 struct RenderFwdArgs {
     const float4* records;     // render records (record_f4), used by the default-shader kernel
@@ -98,7 +125,7 @@ struct RenderBwdArgs {
     int S, W, H, grid_x, grid_y, num_tiles, cull, backward_geometry, RS;
     const uint32_t* tile_order;  // launch order of the tiles (longest first), or null
     float* rows;               // [4L, RS] partial rows (part_row_stride)
-    uint8_t* flags;            // [4L] 1 where a partial row was written (zeroed by the forward's duplicate pass)
+    uint8_t* flags;            // [4L] 1 where a partial row was written (zeroed by the forward's binning scatter)
     const uint8_t* contrib;    // [L] the forward's contribution bits (RenderFwdArgs::contrib)
 };
 
@@ -161,11 +188,10 @@ struct IntermediateArgs {
 // kernels (defined in the .hip translation units)
 __global__ void preprocess_kernel(PreprocessArgs a);
 __global__ void mark_visible_kernel(int P, const float* means3D, const float* view, uint8_t* present);
-__global__ void duplicate_kernel(int P, const uint32_t* offsets, const float2* means2D, const int* radii, int grid_x,
-                                 int grid_y, uint32_t* tile_keys, uint32_t* gid_out, uint32_t* flags, float4* records,
-                                 int rec4);
-__global__ void tile_ranges_kernel(int T, int L, const uint32_t* tiles, uint2* ranges);
-hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint32_t* depth_keys,
+// counts, tile ranges, the longest-first tile order and every workgroup's scatter positions
+hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st);
+hipError_t launch_bin_scatter(const BinArgs& a, hipStream_t st);
+hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint2* pairs,
                                   uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB, hipStream_t st);
 
 // Slot of an instance from its Gaussian's render record word 1 (x, y, slot0, radius) and its tile.
@@ -202,7 +228,7 @@ hipError_t launch_sh_grad_views(int g0, int n, int deg, int M, int N, const floa
 // render record the blend kernels stage from: float4 [conic.x, conic.y, conic.z, opacity],
 // float4 [x, y, slot0 bits, radius bits], then the attribute row [r, g, b, depth, f0 .. f_{SMAX-1}]
 // zero-padded to (4 + SMAX + 3) / 4 float4. slot0 = offsets[g-1] (the Gaussian's first unsorted
-// slot). Written by preprocess_kernel (+ slot0 by duplicate_kernel) for visible
+// slot). Written by preprocess_kernel (+ slot0 by the binning scatter) for visible
 // Gaussians only; the blend kernels never stage an invisible one.
 __host__ __device__ inline int smax_of(int S) {
     return S == 0 ? 0 : S <= 4 ? 4 : S <= 8 ? 8 : S <= 12 ? 12 : S <= 16 ? 16 : S <= 24 ? 24 : 32;
@@ -232,7 +258,6 @@ __device__ __forceinline__ int block_tile(const uint32_t* order, int num_tiles) 
     if (order) return b < num_tiles ? (int)order[b] : num_tiles;
     return xcd_tile(b, gridDim.x);
 }
-__global__ void tile_order_kernel(int T, const uint2* ranges, uint32_t* order);
 #ifdef R3DG_EXP_COUNT  // timing/counting experiment builds only (tools/exp_build.sh)
 static __device__ unsigned long long g_exp_cnt[8];  // one copy per translation unit
 #define R3DG_EXP_READER(name)                                                        \

@@ -6,8 +6,9 @@
 //     every call, rasterize_points.cu:117-122, only so shaders may mutate them);
 //   * no RenderIntermediateTextures pass and no splat-shader launch when the splat shaders are
 //     the defaults (their only outputs are then a stencil of zeros and shader_rgb == rgb);
-//   * rocprim inclusive scan + stable LSD radix sort on bits [0, 32 + msb(tiles)) with the
-//     unsorted slot as the sorted value (see preprocess.hip duplicate_keys_kernel);
+//   * rocprim inclusive scan, then binning by per-tile counters (counting and range passes
+//     overlapped with the num_rendered readback) and a per-tile sort by (depth bits, Gaussian id)
+//     instead of a radix sort of L 64-bit keys (preprocess.hip bin_count_kernel);
 //   * one blocking D2H read of num_rendered, as the reference (rasterizer_impl.cu:347).
 #include <cstring>  // before rocprim on ROCm 7.2
 #include <rocprim/rocprim.hpp>
@@ -56,18 +57,6 @@ static size_t scan_temp_size(size_t P) {
     return bytes;
 }
 
-// Always the onesweep radix sort: rocprim's default switches to a merge sort below 2^20 items,
-// which is several times slower for the 1M-Gaussian depth sort.
-using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                              rocprim::default_config, 0>;
-
-static size_t sort_temp_size(size_t L) {  // tile sort of the instances
-    size_t bytes = 0;
-    uint32_t* k = nullptr;
-    rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, k, k, k, k, L, 0, 32, 0);
-    return bytes;
-}
-
 static bool use_tile_order() {
     const char* e = getenv("R3DG_TILE_ORDER");
     return !(e && e[0] == 'x');  // backward: "xcd" = spatial XCD-aware order; default longest first
@@ -112,15 +101,13 @@ GeomState geom_state_from(void* base, size_t P, int S) { return carve_geom((uint
 
 static BinningState carve_binning(uintptr_t p, size_t L, uintptr_t* end) {
     BinningState b{};
-    b.tile_keys = carve<uint32_t>(p, L);
-    b.tile_sorted = carve<uint32_t>(p, L);
-    b.gid_in = carve<uint32_t>(p, L);
     b.point_list = carve<uint32_t>(p, L);
-    b.keys2 = carve<uint32_t>(p, L);
+    b.pairs = carve<uint2>(p, L);
+    b.sort_k1 = carve<uint32_t>(p, L);
+    b.sort_v1 = carve<uint32_t>(p, L);
+    b.sort_k2 = carve<uint32_t>(p, L);
     b.flags = carve<uint32_t>(p, L);
     b.contrib = carve<uint8_t>(p, L);
-    b.sort_temp_bytes = sort_temp_size(L);
-    b.sort_temp = carve<char>(p, b.sort_temp_bytes);
     if (end) *end = p;
     return b;
 }
@@ -141,6 +128,8 @@ static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end) {
     const size_t T = (size_t)num_tiles_of(H, W);
     s.ranges = carve<uint2>(p, T);
     s.tile_order = carve<uint32_t>(p, T);
+    s.tile_work = carve<uint32_t>(p, T);
+    s.bin_hist = carve<uint32_t>(p, (size_t)bin_blocks_max((int)T) * T);
     if (end) *end = p;
     return s;
 }
@@ -223,18 +212,6 @@ static hipError_t readback_slot(Readback** out) {
     }
     *out = &r;
     return hipSuccess;
-}
-
-// rasterizer_impl.cu:37-52
-static uint32_t higher_msb(uint32_t n) {
-    uint32_t msb = sizeof(n) * 4, step = msb;
-    while (step > 1) {
-        step /= 2;
-        if (n >> msb) msb += step;
-        else msb -= step;
-    }
-    if (n >> msb) msb++;
-    return msb;
 }
 
 // InitializeStencil (rasterizer_impl.cu:203-209)
@@ -543,6 +520,17 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     }
 
     int L = 0;
+    BinArgs binning{};
+    binning.P = P; binning.grid_x = gx; binning.grid_y = gy; binning.rec4 = record_f4(S); binning.T = T;
+    binning.offsets = geom.point_offsets; binning.means2D = geom.means2D; binning.radii = radii;
+    binning.depth_keys = geom.depth_keys;
+    binning.tile_work = img.tile_work; binning.records = geom.records;
+    {
+        const char* e = getenv("R3DG_BIN");  // "atomic": the global-atomic binning (tests)
+        const bool lds = bin_blocks_max(T) > 0 && !(e && e[0] == 'a');
+        binning.nblk = lds ? std::min(bin_blocks_max(T), (P + kBinSub - 1) / kBinSub) : 0;
+        binning.hist = lds && P > 0 ? img.bin_hist : nullptr;
+    }
     if (P > 0) {
         PreprocessArgs pa{};
         pa.P = P; pa.D = s->D; pa.M = s->M; pa.W = W; pa.H = H; pa.grid_x = gx; pa.grid_y = gy;
@@ -557,6 +545,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         pa.depths = geom.depths;
         pa.means2D = geom.means2D; pa.cov3D = geom.cov3D; pa.conic_opacity = geom.conic_opacity;
         pa.rgb = geom.rgb; pa.clamped = geom.clamped; pa.error_flag = nullptr;
+        pa.tile_count = binning.hist ? nullptr : img.tile_work;  // the atomic binning's counters
+        pa.num_tiles = T;
         Readback* rb = nullptr;
         R3DG_CHECK_HIP(readback_slot(&rb));
         if (s->prefiltered) {
@@ -583,6 +573,13 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         if (s->prefiltered)
             R3DG_CHECK_HIP(hipMemcpyAsync(rb->host + 1, rb->dev_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         R3DG_CHECK_HIP(hipEventRecord(rb->ev, st));
+        // binning passes that need only the scan: per-tile counts, ranges, the tile order and the
+        // scatter positions run on the device while the host waits for num_rendered and allocates
+        {
+            ProfScope ps(R3DG_PROF_SORT, st, true);
+            R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, st));
+            R3DG_CHECK_LAUNCH(s->debug, st);
+        }
         R3DG_CHECK_HIP(hipEventSynchronize(rb->ev));
         const uint32_t Lh = *rb->host;
         R3DG_REQUIRE(!s->prefiltered || rb->host[1] == 0,
@@ -590,6 +587,10 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
                      "auxiliary.h:156-160)");
         R3DG_REQUIRE(Lh < (1u << 31), "rasterize_gaussians: too many tile instances");
         L = (int)Lh;
+    } else if (T > 0) {  // no Gaussians: every tile range empty
+        R3DG_CHECK_HIP(hipMemsetAsync(img.tile_work, 0, sizeof(uint32_t) * (size_t)T, st));
+        R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, st));
+        R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
     void* bin_base = binning_alloc(binning_ctx, binning_state_bytes((size_t)L));
@@ -599,36 +600,16 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     }
     BinningState bin = binning_state_from(bin_base, (size_t)L);
     if (L > 0) {
-        // duplicateWithKeys in the reference's Gaussian-major slot order (also zeroes the
-        // backward's row flags), stable sort by tile over bits [0, msb(T)), then every tile stably
-        // by depth: the reference's 45-bit stable sort of (tile << 32 | depth bits)
-        // (rasterizer_impl.cu:366-374) without a 64-bit key over L
-        hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, geom.point_offsets,
-                           geom.means2D, radii, gx, gy, bin.tile_keys, bin.gid_in, bin.flags, geom.records,
-                           record_f4(S));
-        R3DG_CHECK_LAUNCH(s->debug, st);
-        const int bit = (int)higher_msb((uint32_t)T);
-        size_t sb = bin.sort_temp_bytes;
-        {
-            ProfScope ps(R3DG_PROF_SORT, st, true);
-            R3DG_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(bin.sort_temp, sb, bin.tile_keys, bin.tile_sorted,
-                                                                 bin.gid_in, bin.point_list, (size_t)L, 0, bit, st));
-        }
-    }
-    // tile ranges for every tile (empty ones included: no memset), then the longest-first tile
-    // order the depth sort and the backward launch in
-    const bool order_tiles = use_tile_order();
-    if (T > 0) {
-        hipLaunchKernelGGL(tile_ranges_kernel, dim3((T + 255) / 256), dim3(256), 0, st, T, L, bin.tile_sorted,
-                           img.ranges);
-        R3DG_CHECK_LAUNCH(s->debug, st);
-        hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, T, img.ranges, img.tile_order);
-        R3DG_CHECK_LAUNCH(s->debug, st);
-    }
-    if (L > 0) {
+        // every instance to its tile's next position (also zeroes the backward's row flags and
+        // records each Gaussian's first slot), then every tile by (depth bits, Gaussian id): the
+        // reference's 45-bit stable sort of (tile << 32 | depth bits) (rasterizer_impl.cu:366-374)
         ProfScope ps(R3DG_PROF_SORT, st, true);
-        R3DG_CHECK_HIP(launch_tile_depth_sort(T, img.ranges, img.tile_order, geom.depth_keys, bin.point_list,
-                                              bin.tile_keys, bin.gid_in, bin.keys2, st));
+        binning.pairs = bin.pairs;
+        binning.flags = bin.flags;
+        R3DG_CHECK_HIP(launch_bin_scatter(binning, st));
+        R3DG_CHECK_LAUNCH(s->debug, st);
+        R3DG_CHECK_HIP(launch_tile_depth_sort(T, img.ranges, img.tile_order, bin.pairs, bin.point_list,
+                                              bin.sort_k1, bin.sort_v1, bin.sort_k2, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
@@ -675,7 +656,6 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     ra.bg = s->bg;
     ra.S = S; ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = T; ra.cull = 1;
     ra.tile_order = nullptr;  // forward: XCD-aware spatial order (measured faster: L2 locality)
-    (void)order_tiles;
     ra.final_T = img.final_T;
     ra.n_contrib = img.n_contrib;
     ra.out_color = out->color;
@@ -732,7 +712,6 @@ extern "C" int r3dg_state_view(int P, int H, int W, int L, void* geom, void* bin
     GeomState gs = geom_state_from(geom, (size_t)P);
     BinningState bs = binning_state_from(binning, (size_t)L);
     ImageState is = image_state_from(image, H, W);
-    v->tile_sorted = bs.tile_sorted;
     v->point_list = bs.point_list;
     v->ranges = reinterpret_cast<const uint32_t*>(is.ranges);
     v->point_offsets = gs.point_offsets;

@@ -558,11 +558,9 @@ std::vector<torch::Tensor> rasterizer_state(const torch::Tensor& geomBuffer, con
     // the reference's sort key, rebuilt: tile << 32 | float bits of the instance's depth
     auto plist = slice(binningBuffer, v.point_list, 4 * L).view(torch::kInt32);
     auto dbits = slice(geomBuffer, v.depths, 4 * P).view(torch::kInt32).to(torch::kInt64).bitwise_and(0xffffffffLL);
-    auto keys = slice(binningBuffer, v.tile_sorted, 4 * L)
-                    .view(torch::kInt32)
-                    .to(torch::kInt64)
-                    .bitwise_left_shift(32)
-                    .bitwise_or(dbits.index_select(0, plist.to(torch::kInt64)));
+    auto rng = slice(imageBuffer, v.ranges, 8 * T).view(torch::kInt32).view({T, 2}).to(torch::kInt64);
+    auto tiles = torch::repeat_interleave(torch::arange(T, rng.options()), rng.select(1, 1) - rng.select(1, 0), 0, L);
+    auto keys = tiles.bitwise_left_shift(32).bitwise_or(dbits.index_select(0, plist.to(torch::kInt64)));
     return {keys,
             plist,
             slice(imageBuffer, v.ranges, 8 * T).view(torch::kInt32).view({T, 2}),

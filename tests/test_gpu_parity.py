@@ -331,21 +331,17 @@ def test_sh_degrees(hip_ext):
         assert_close(f"dL_dsh deg{deg}", gh["dL_dsh"], go["dL_dsh"], _grad_tol(go["dL_dsh"]), 2e-3)
 
 
-def test_m1_keys_full_size(hip_ext):
-    """BASELINE.json metric config (1M Gaussians, 1920x1080): keys and sort order bit-exact vs the
-    oracle's preprocess + stable LSD sort; blend invariants checked on the full image."""
-    import relightable3dgaussian_amd as r
-
-    cam = synthetic.m1_camera()
-    scene = synthetic.m1_scene(P=1_000_000, S=11, seed=0, cam=cam)
-    h = hip_forward(hip_ext, scene, cam, S=11)
-    L = h["num_rendered"]
-    assert 4_000_000 < L < 6_500_000
-    st = r._C.rasterizer_state(h["geom"], h["binning"], h["image"], scene.P, cam.height, cam.width, L)
-    keys = st[0].cpu().numpy().view(np.uint64)
-    assert np.all(keys[1:] >= keys[:-1])  # sorted
+def _keys_vs_oracle(hip_ext, scene, cam, h):
+    """Sorted keys (tile << 32 | depth bits) and point list of a HIP forward against the oracle's
+    preprocess + duplicateWithKeys + stable sort (rasterizer_impl.cu:343-383); ranges against the
+    boundaries of the sorted keys."""
     import ctypes
 
+    import relightable3dgaussian_amd as r
+
+    L = h["num_rendered"]
+    st = r._C.rasterizer_state(h["geom"], h["binning"], h["image"], scene.P, cam.height, cam.width, L)
+    keys = st[0].cpu().numpy().view(np.uint64)
     lib = oracle.lib()
     P = scene.P
     F = np.float32
@@ -369,6 +365,23 @@ def test_m1_keys_full_size(hip_ext):
     order = np.lexsort((np.arange(L), okeys))  # stable sort by key
     np.testing.assert_array_equal(keys, okeys[order])
     np.testing.assert_array_equal(st[1].cpu().numpy().view(np.uint32), ovals[order])
+    T = ((cam.width + 15) // 16) * ((cam.height + 15) // 16)
+    tiles = (okeys[order] >> np.uint64(32)).astype(np.int64)
+    lo = np.searchsorted(tiles, np.arange(T), "left")
+    hi = np.searchsorted(tiles, np.arange(T), "right")
+    rng = np.where((hi > lo)[:, None], np.stack([lo, hi], 1), 0)
+    np.testing.assert_array_equal(st[2].cpu().numpy().astype(np.int64), rng)
+    return L
+
+
+def test_m1_keys_full_size(hip_ext):
+    """BASELINE.json metric config (1M Gaussians, 1920x1080): keys, sort order and ranges bit-exact
+    vs the oracle's preprocess + stable sort; blend invariants checked on the full image."""
+    cam = synthetic.m1_camera()
+    scene = synthetic.m1_scene(P=1_000_000, S=11, seed=0, cam=cam)
+    h = hip_forward(hip_ext, scene, cam, S=11)
+    L = _keys_vs_oracle(hip_ext, scene, cam, h)
+    assert 4_000_000 < L < 6_500_000
     import torch
 
     op = h["opacity"].cpu().numpy()[..., 0].reshape(-1)
@@ -386,6 +399,39 @@ def _brdf_tensors(inp):
 
     return [tt(inp[k]) for k in ["base", "rough", "metal", "normals", "viewdirs", "incidents", "env", "visibility"]]
 
+
+
+@pytest.mark.parametrize("size", [(3200, 1800), (4200, 2400)])
+def test_binning_large_frames(hip_ext, size):
+    """Binning above 12288 tiles (3200x1800: 22600 tiles, LDS counters beyond 64 KiB per workgroup)
+    and above kBinMaxTiles (4200x2400: 39450 tiles, the global-atomic fallback): keys, point list
+    and ranges bit-exact vs the oracle."""
+    cam = synthetic.m1_camera(*size)
+    scene = synthetic.m1_scene(P=150_000, S=3, seed=5, cam=cam)
+    h = hip_forward(hip_ext, scene, cam, S=3)
+    assert _keys_vs_oracle(hip_ext, scene, cam, h) > 100_000
+
+
+def test_binning_atomic_path_matches(hip_ext):
+    """The global-atomic binning (R3DG_BIN=atomic, the fallback above kBinMaxTiles) and the LDS
+    binning give bit-identical sorted lists, images and gradients; both match the oracle's keys."""
+    cam = synthetic.m1_camera(480, 272)
+    scene = synthetic.m1_scene(P=60_000, S=11, seed=9, cam=cam)
+    a = hip_forward(hip_ext, scene, cam, S=11)
+    _keys_vs_oracle(hip_ext, scene, cam, a)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=2)
+    ga = hip_backward(hip_ext, a, dc, do, dd, df)
+    os.environ["R3DG_BIN"] = "atomic"
+    try:
+        b = hip_forward(hip_ext, scene, cam, S=11)
+        gb = hip_backward(hip_ext, b, dc, do, dd, df)
+    finally:
+        del os.environ["R3DG_BIN"]
+    _keys_vs_oracle(hip_ext, scene, cam, b)
+    for k in ["color", "opacity", "depth", "feature", "n_contrib"]:
+        np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
+    for k in ga:
+        np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
 
 def test_brdf_complex_matches_oracle_and_golden(hip_ext):
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "brdf_pi5.npz"))
