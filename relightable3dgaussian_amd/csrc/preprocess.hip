@@ -7,10 +7,9 @@
 // the keys and the sort order are reproducible (SURVEY.md §7 "Bit-exact keys").
 #pragma clang fp contract(off)
 
-#include <rocprim/block/block_radix_sort.hpp>
-
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
+#include "r3dg_tilesort.h"
 
 #ifndef R3DG_SORT_LONG_IPT
 #define R3DG_SORT_LONG_IPT 8  // items per thread of the depth sort for tiles longer than 1024 instances
@@ -543,13 +542,9 @@ hipError_t launch_bin_scatter(const BinArgs& a, hipStream_t st) {
 // Gaussian id, then stably by depth. A tile longer than one chunk sorts each chunk into a run and
 // merges run pairs (merge path, (depth, id) compared lexicographically) through the scratch
 // buffers, ping-pong, landing in point_list.
-constexpr int kSortBT = 256;
-using TileDepthSort4 = rocprim::block_radix_sort<uint32_t, kSortBT, 4, uint32_t>;
-using TileDepthSortL = rocprim::block_radix_sort<uint32_t, kSortBT, R3DG_SORT_LONG_IPT, uint32_t>;
 union TileDepthSortStorage {
-    typename TileDepthSort4::storage_type s4;
-    typename TileDepthSortL::storage_type sl;
-    uint32_t keys[kSortBT * R3DG_SORT_LONG_IPT];  // the sorted chunk's keys (tie test)
+    TileSortLds<4> s4;
+    TileSortLds<R3DG_SORT_LONG_IPT> sl;
 };
 
 __device__ __forceinline__ uint32_t nt_load(const uint32_t* p) { return __builtin_nontemporal_load(p); }
@@ -560,10 +555,9 @@ __device__ __forceinline__ bool kv_less(uint32_t ka, uint32_t va, uint32_t kb, u
 }
 
 // chunks of kSortBT * IPT instances of the tile [s, s + n) sorted into runs at (rk, rv)
-template <int IPT, class Sort, class Storage>
+template <int IPT>
 __device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_t nchunks, const uint2* pairs,
-                                                 uint32_t* rk, uint32_t* rv,
-                                                 TileDepthSortStorage& st, Storage& storage) {
+                                                 uint32_t* rk, uint32_t* rv, TileSortLds<IPT>& lds) {
     constexpr uint32_t kChunk = kSortBT * IPT;
     const int t = threadIdx.x;
     for (uint32_t c = 0; c < nchunks; ++c) {
@@ -572,29 +566,12 @@ __device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {  // blocked arrangement: item index = t * IPT + k
             const uint32_t i = c0 + (uint32_t)(t * IPT + k);
-            // visible depths < 0x7f800000: pads sort last
             const uint2 kv = i < n ? pairs[s + i] : make_uint2(0xffffffffu, 0xffffffffu);
             keys[k] = kv.x;
             vals[k] = kv.y;
         }
         if (c > 0) __syncthreads();  // storage reuse
-        Sort().sort(keys, vals, storage, 0, 32);
-        // equal depth bits anywhere in the chunk (pads excluded: they are the all-ones key)?
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < IPT; ++k) st.keys[t * IPT + k] = keys[k];
-        __syncthreads();
-        bool tie = false;
-#pragma unroll
-        for (int k = 0; k < IPT; ++k) {
-            const int i = t * IPT + k;
-            if (i + 1 < (int)kChunk && keys[k] != 0xffffffffu && st.keys[i + 1] == keys[k]) tie = true;
-        }
-        if (__syncthreads_or(tie)) {  // block-uniform: id order first, then stably by depth
-            Sort().sort(vals, keys, storage, 0, 32);
-            __syncthreads();
-            Sort().sort(keys, vals, storage, 0, 32);
-        }
+        sort_pairs_chunk<IPT>(keys, vals, (int)min(kChunk, n - c0), lds);
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const uint32_t i = c0 + (uint32_t)(t * IPT + k);
@@ -606,10 +583,10 @@ __device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_
     }
 }
 
-__global__ void __launch_bounds__(kSortBT) __attribute__((amdgpu_waves_per_eu(8)))
+__global__ void __launch_bounds__(kSortBT)
 tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges, const uint32_t* __restrict__ order,
                        const uint2* __restrict__ pairs, uint32_t* __restrict__ point_list,
-                       uint32_t* kA, uint32_t* vA, uint32_t* kB) {
+                       uint32_t* kA, uint32_t* vA, uint32_t* kB, int min_n) {
     __shared__ TileDepthSortStorage storage;
     const int b = blockIdx.x;
     if (b >= T) return;
@@ -617,8 +594,9 @@ tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges, const uint32_t* 
     const uint2 rg = ranges[tile];
     const uint32_t s = rg.x, n = rg.y - rg.x;
     const int t = threadIdx.x;
-    if (n <= 1) {
-        if (n == 1 && t == 0) point_list[s] = pairs[s].y;
+    if (n <= (uint32_t)min_n) return;  // sorted by the forward blend (fused)
+    if (n == 1) {
+        if (t == 0) point_list[s] = pairs[s].y;
         return;
     }
     // sorter capacity by tile length (block-uniform); a 2-item sorter for tiles of up to 512
@@ -631,10 +609,9 @@ tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges, const uint32_t* 
     uint32_t* rk = (rounds & 1) ? kA : kB;
     uint32_t* rv = (rounds & 1) ? vA : point_list;
     if (kChunk == kSortBT * 4)
-        sort_tile_chunks<4, TileDepthSort4>(s, n, nchunks, pairs, rk, rv, storage, storage.s4);
+        sort_tile_chunks<4>(s, n, nchunks, pairs, rk, rv, storage.s4);
     else
-        sort_tile_chunks<R3DG_SORT_LONG_IPT, TileDepthSortL>(s, n, nchunks, pairs, rk, rv, storage,
-                                                             storage.sl);
+        sort_tile_chunks<R3DG_SORT_LONG_IPT>(s, n, nchunks, pairs, rk, rv, storage.sl);
     if (nchunks == 1) return;
     __syncthreads();
     uint32_t *sk = rk, *sv = rv, *dk = (rk == kA) ? kB : kA, *dv = (rk == kA) ? point_list : vA;
@@ -683,10 +660,10 @@ tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges, const uint32_t* 
 
 hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint2* pairs,
                                   uint32_t* point_list, uint32_t* kA, uint32_t* vA,
-                                  uint32_t* kB, hipStream_t st) {
+                                  uint32_t* kB, int min_n, hipStream_t st) {
     if (T <= 0) return hipSuccess;
     hipLaunchKernelGGL(tile_depth_sort_kernel, dim3(T), dim3(kSortBT), 0, st, T, ranges, order, pairs, point_list,
-                       kA, vA, kB);
+                       kA, vA, kB, min_n);
     return hipGetLastError();
 }
 

@@ -86,7 +86,13 @@ struct RenderFwdArgs {
     float* zero_stencil;  // stencil output to zero (default splat shaders), or null
     uint8_t* contrib;     // [L] per sorted position: bit q set when a pixel of quadrant q blended it
     FeatureLayout flay;
+    // fused depth sort (default-shader kernel): tiles of up to kFusedSortMax instances are sorted
+    // from the binning's (depth bits, id) pairs in the blend's prologue and their sorted ids written
+    // to point_list_out; null pairs: every tile was sorted by tile_depth_sort_kernel
+    const uint2* pairs;
+    uint32_t* point_list_out;
 };
+constexpr int kFusedSortMax = 1024;
 
 // Per-Gaussian gradient sums the gather kernel assembles (LDS, one row per Gaussian):
 // [mean2D x,y,z | conic x,y,w | opacity | colour r,g,b | features 0..S-1 | pad].
@@ -191,8 +197,10 @@ __global__ void mark_visible_kernel(int P, const float* means3D, const float* vi
 // counts, tile ranges, the longest-first tile order and every workgroup's scatter positions
 hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st);
 hipError_t launch_bin_scatter(const BinArgs& a, hipStream_t st);
+// sorts the tiles longer than min_n instances (the forward sorts the others when fused)
 hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint2* pairs,
-                                  uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB, hipStream_t st);
+                                  uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB, int min_n,
+                                  hipStream_t st);
 
 // Slot of an instance from its Gaussian's render record word 1 (x, y, slot0, radius) and its tile.
 __device__ __forceinline__ uint32_t record_slot(float4 r1, int tx, int ty, int grid_x, int grid_y) {

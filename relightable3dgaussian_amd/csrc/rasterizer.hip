@@ -608,8 +608,10 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
         binning.flags = bin.flags;
         R3DG_CHECK_HIP(launch_bin_scatter(binning, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
+        // the default-shader blend sorts the tiles of up to kFusedSortMax instances itself
         R3DG_CHECK_HIP(launch_tile_depth_sort(T, img.ranges, img.tile_order, bin.pairs, bin.point_list,
-                                              bin.sort_k1, bin.sort_v1, bin.sort_k2, st));
+                                              bin.sort_k1, bin.sort_v1, bin.sort_k2,
+                                              splat_active ? 0 : kFusedSortMax, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
@@ -668,6 +670,8 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     // the blend writes those zeros with its other outputs (no separate memset launch)
     ra.zero_stencil = splat_active ? nullptr : out->stencil;
     ra.contrib = bin.contrib;
+    ra.pairs = splat_active ? nullptr : bin.pairs;  // fused depth sort (render_fwd_glds_kernel)
+    ra.point_list_out = bin.point_list;
     if (const char* e = getenv("R3DG_NO_CULL")) ra.cull = (e[0] == '0');
     {
         ProfScope ps(R3DG_PROF_RENDER_FWD, st);

@@ -17,6 +17,7 @@
 // render_fwd_shader_kernel blends the splat-shader colour as well (non-default splat shaders).
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
+#include "r3dg_tilesort.h"
 
 namespace r3dg {
 
@@ -57,7 +58,6 @@ render_fwd_shader_kernel(RenderFwdArgs a) {
     const float pfx = (float)px, pfy = (float)py;
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
-
     bool done = !inside;
     float T = 1.0f;
     uint32_t last = 0;
@@ -228,9 +228,13 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     constexpr int SBUF = RF4 * NB;             // float4 per staging buffer
     constexpr int NCP = RF4 * NH;              // DMA wave-instructions per batch
     static_assert(NB == 64, "one 64-bit contribution word per wave and batch");
-    // one LDS array: [2 staging buffers | 2 x 64 x 4 contribution flags (batch buffer, instance, wave)]
-    __shared__ float4 s_lds[2 * SBUF + 32];
-    uint8_t* const s_cf = reinterpret_cast<uint8_t*>(s_lds + 2 * SBUF);
+    // one LDS array: [2 staging buffers | 2 x 64 x 4 contribution flags (batch buffer, instance, wave)
+    // | the tile's sorted Gaussian ids (fused sort)]; the fused sort's scratch aliases the staging
+    constexpr int SORT4 = (int)((sizeof(TileSortLds<kFusedSortMax / kSortBT>) + 15) / 16);
+    constexpr int STG = 2 * SBUF > SORT4 ? 2 * SBUF : SORT4;  // float4 of staging / sort scratch
+    __shared__ float4 s_lds[STG + 32 + kFusedSortMax / 4];
+    uint8_t* const s_cf = reinterpret_cast<uint8_t*>(s_lds + STG);
+    uint32_t* const s_ids = reinterpret_cast<uint32_t*>(s_lds + STG + 32);
     if (threadIdx.x < 128) reinterpret_cast<uint32_t*>(s_cf)[threadIdx.x] = 0u;  // before the first barrier
 
     const int tile = block_tile(a.tile_order, a.num_tiles);
@@ -245,6 +249,32 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
 
+    // fused depth sort (block-uniform): the tile's (depth bits, id) pairs sorted in the prologue
+    // (r3dg_tilesort.h), ids kept in LDS for the staging and written out for the backward; saves
+    // the standalone sort launch, whose time is its barriers' latency, not its work
+    const bool fused = a.pairs != nullptr && n <= kFusedSortMax;
+    if (fused && n > 0) {
+        constexpr int IPT = kFusedSortMax / kSortBT;
+        uint32_t keys[IPT], vals[IPT];
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const int i = t * IPT + k;
+            const uint2 kv = i < n ? a.pairs[range.x + i] : make_uint2(0xffffffffu, 0xffffffffu);
+            keys[k] = kv.x;
+            vals[k] = kv.y;
+        }
+        if (n > 1) sort_pairs_chunk<IPT>(keys, vals, n, *reinterpret_cast<TileSortLds<IPT>*>(s_lds));
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            const int i = t * IPT + k;
+            if (i < n) {
+                s_ids[i] = vals[k];
+                a.point_list_out[range.x + i] = vals[k];
+            }
+        }
+        __syncthreads();
+    }
+
     bool done = !inside;
     float T = 1.0f;
     uint32_t last = 0;
@@ -257,7 +287,10 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     // the tile's last instance, so every DMA lane reads a valid record)
     auto load_gids = [&](int b0, uint32_t (&gd)[NH]) {
 #pragma unroll
-        for (int h = 0; h < NH; ++h) gd[h] = a.point_list[range.x + (uint32_t)min(b0 + h * 64 + l, n - 1)];
+        for (int h = 0; h < NH; ++h) {
+            const int i = min(b0 + h * 64 + l, n - 1);
+            gd[h] = fused ? s_ids[i] : a.point_list[range.x + (uint32_t)i];
+        }
     };
     // the DMA is inline asm: the compiler does not wait for it before the LDS reads of the other
     // buffer; the batch loop waits for it explicitly (vmcnt(0) before the batch barrier)

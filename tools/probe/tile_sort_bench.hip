@@ -24,10 +24,11 @@
 // MODE 1: rocPRIM block radix sort, bits [0, 32)
 // MODE 2: same, bits trimmed to the tile's varying range (block OR/AND reduction first)
 // MODE 3: 64-bit (depth << 32 | gid) keys over [0, 52) (what an unordered scatter would need)
-template <int BS, int IPT, int MODE>
+template <int BS, int IPT, int MODE, int RB = 0,
+          rocprim::block_radix_rank_algorithm ALG = rocprim::block_radix_rank_algorithm::default_for_radix_sort>
 __global__ void __launch_bounds__(BS) sort_kernel(int T, const uint2* ranges, const uint32_t* depth_keys,
                                                   uint32_t* plist) {
-    using Sort32 = rocprim::block_radix_sort<uint32_t, BS, IPT, uint32_t>;
+    using Sort32 = rocprim::block_radix_sort<uint32_t, BS, IPT, uint32_t, 1, 1, RB, ALG>;
     using Sort64 = rocprim::block_radix_sort<uint64_t, BS, IPT>;
     __shared__ union {
         typename Sort32::storage_type s32;
@@ -142,6 +143,17 @@ int main() {
     timeit("rocprim 32b 512x2", sort_kernel<512, 2, 1>, T, dr, ddk, dpl, dpl0, L, 512);
     timeit("rocprim 32b 128x8", sort_kernel<128, 8, 1>, T, dr, ddk, dpl, dpl0, L, 128);
     timeit("rocprim 32b 1024x1", sort_kernel<1024, 1, 1>, T, dr, ddk, dpl, dpl0, L, 1024);
+    using A = rocprim::block_radix_rank_algorithm;
+    timeit("match rb4 256x4", sort_kernel<256, 4, 1, 4, A::match>, T, dr, ddk, dpl, dpl0, L, 256);
+    timeit("match rb6 256x4", sort_kernel<256, 4, 1, 6, A::match>, T, dr, ddk, dpl, dpl0, L, 256);
+    timeit("match rb8 256x4", sort_kernel<256, 4, 1, 8, A::match>, T, dr, ddk, dpl, dpl0, L, 256);
+    timeit("match rb11 256x4", sort_kernel<256, 4, 1, 11, A::match>, T, dr, ddk, dpl, dpl0, L, 256);
+    timeit("basic rb4 256x4", sort_kernel<256, 4, 1, 4, A::basic>, T, dr, ddk, dpl, dpl0, L, 256);
+    timeit("memoize rb4 256x4", sort_kernel<256, 4, 1, 4, A::basic_memoize>, T, dr, ddk, dpl, dpl0, L, 256);
+    timeit("memoize rb8 256x4", sort_kernel<256, 4, 1, 8, A::basic_memoize>, T, dr, ddk, dpl, dpl0, L, 256);
+    timeit("match rb8 128x8", sort_kernel<128, 8, 1, 8, A::match>, T, dr, ddk, dpl, dpl0, L, 128);
+    timeit("match rb11 128x8", sort_kernel<128, 8, 1, 11, A::match>, T, dr, ddk, dpl, dpl0, L, 128);
+    timeit("match rb8 64x16", sort_kernel<64, 16, 1, 8, A::match>, T, dr, ddk, dpl, dpl0, L, 64);
     timeit("rocprim 64b(52) 256x4", sort_kernel<256, 4, 3>, T, dr, ddk, dpl, dpl0, L, 256);
     CK(hipMemcpy(o2.data(), dpl, 4 * L, hipMemcpyDeviceToHost));
     printf("  64b == 32b stable: %d\n", (int)(o2 == ref));
