@@ -528,7 +528,9 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     {
         const char* e = getenv("R3DG_BIN");  // "atomic": the global-atomic binning (tests)
         const bool lds = bin_blocks_max(T) > 0 && !(e && e[0] == 'a');
-        binning.nblk = lds ? std::min(bin_blocks_max(T), (P + kBinSub - 1) / kBinSub) : 0;
+        int nb = bin_blocks_max(T);
+        if (const char* eb = getenv("R3DG_BIN_BLOCKS")) nb = std::max(1, std::min(nb, atoi(eb)));  // experiments
+        binning.nblk = lds ? std::min(nb, (P + kBinSub - 1) / kBinSub) : 0;
         binning.hist = lds && P > 0 ? img.bin_hist : nullptr;
     }
     if (P > 0) {
