@@ -14,7 +14,8 @@ renders its own camera of the same scene (weak scaling).
 
 Rank 0 prints one JSON line. `roofline` prices renderCUDA fwd + bwd -- render_fwd_glds_kernel,
 render_bwd_glds_kernel and row_sum_kernel (the backward's per-instance reduction) -- with SURVEY.md
-§8d's algorithmic bytes (272*L + 156*H*W + 16*tiles at S=11) over their device time, from HIP
+§8d's algorithmic bytes (272*L + 156*H*W + 16*tiles at S=11, + 12*L for the depth sort fused into the
+forward) over their device time, from HIP
 events recorded inside each launch's dispatch on the launch stream during K further steps (the
 timed K steps run without events);
 `traffic` is the HBM bytes of the same kernels from rocprofv3 PMC counters (profiles/, FETCH_SIZE
@@ -42,8 +43,10 @@ P_M1, W_M1, H_M1, S_M1 = 1_000_000, 1920, 1080, 11
 
 
 def algorithmic_bytes(L: int, npix: int, tiles: int, S: int) -> tuple[int, int]:
-    """SURVEY.md §8d per-unit figures: fwd L*(56+4S) + Npix*(40+4S) + 8T, bwd L*(84+8S) + Npix*(28+4S) + 8T."""
-    fwd = L * (56 + 4 * S) + npix * (40 + 4 * S) + 8 * tiles
+    """SURVEY.md §8d per-unit figures: fwd L*(56+4S) + Npix*(40+4S) + 8T, bwd L*(84+8S) + Npix*(28+4S) + 8T;
+    plus 12 L for the forward, which also sorts its tiles (the binning's (depth, id) pairs read, the
+    sorted point_list written: render_fwd.hip fused depth sort)."""
+    fwd = L * (56 + 4 * S + 12) + npix * (40 + 4 * S) + 8 * tiles
     bwd = L * (84 + 8 * S) + npix * (28 + 4 * S) + 8 * tiles
     return fwd, bwd
 

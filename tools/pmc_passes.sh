@@ -7,7 +7,7 @@ OUT=gpurun_out/pmc
 mkdir -p $OUT
 run() {
   name=$1; shift
-  timeout -k 10 240 rocprofv3 --pmc "$@" --kernel-include-regex "render_|gather_bwd|row_sum|preprocess_kernel|identify|duplicate" \
+  timeout -k 10 240 rocprofv3 --pmc "$@" --kernel-include-regex "render_|gather_bwd|row_sum|preprocess_kernel|bin_|tile_" \
      -d $OUT/$name -o run --output-format csv -- python tools/step_once.py > $OUT/$name.log 2>&1
 }
 run sq1 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES
