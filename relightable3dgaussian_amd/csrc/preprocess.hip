@@ -583,7 +583,10 @@ __device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_
     }
 }
 
-__global__ void __launch_bounds__(kSortBT)
+#ifndef R3DG_SORT_WAVES
+#define R3DG_SORT_WAVES 6  // waves per SIMD the long-tile sorter's registers target (80 VGPR; 8: 64, spills)
+#endif
+__global__ void __launch_bounds__(kSortBT) __attribute__((amdgpu_waves_per_eu(R3DG_SORT_WAVES)))
 tile_depth_sort_kernel(int T, const uint2* __restrict__ ranges, const uint32_t* __restrict__ order,
                        const uint2* __restrict__ pairs, uint32_t* __restrict__ point_list,
                        uint32_t* kA, uint32_t* vA, uint32_t* kB, int min_n) {
