@@ -102,7 +102,9 @@ constexpr int kRowMean = 0, kRowConic = 3, kRowOpacity = 6, kRowColor = 7, kRowF
 // the reduction of one wave's 64 pixels, at index 4 * slot + quadrant:
 //   [0, XW)      X part: sum_px w * [dL/dcolour 0..2, dL/dfeature 0..S-1, dL/ddepth], zero pad
 //   [XW, XW+6)   moments of q = G * dL/dalpha about the quadrant centre (pixel offsets x, y in
-//                -3.5 .. 3.5): sum q * [1, x, y, x^2, xy, y^2]; then 2 pad floats
+//                -3.5 .. 3.5): sum q * [1, x, y, x^2, xy, y^2]
+//   [XW+6, XW+8) the quadrant centre (pixel coordinates): the row sum expands the moments about
+//                the Gaussian's mean without decoding the row's tile
 // with w = alpha * T and XW = 16 * bwd_xblocks(S). A row exists only where the wave blended the
 // instance; flags[4 * slot + quadrant] = 1 marks it (the gather reads flagged rows only).
 __host__ __device__ inline int bwd_xblocks(int S);

@@ -73,6 +73,21 @@ __device__ __forceinline__ int block_max_last(int wmax, int* s_max_last) {
     return *s_max_last;
 }
 
+// One wave's pixel moments of q, sum q * [1, x, y, x^2, xy, y^2] with (x, y) = pixel - quadrant
+// centre, expanded about the Gaussian's mean: with (d0x, d0y) = mean - quadrant centre the pixel's
+// offset from the mean is (d0x - x, d0y - y), so
+//   sum q dx = d0x S0 - Sx,  sum q dx^2 = d0x^2 S0 - 2 d0x Sx + Sxx,  sum q dx dy = d0x d0y S0 - d0x Sy
+//   - d0y Sx + Sxy  (and y alike): the partial row's moments (r3dg_kernels.h), what
+// backward.cu:583-611 sums per pixel through dG/ddelx, dG/ddely and the conic terms.
+__device__ __forceinline__ void expand_moments(const float (&s)[6], float d0x, float d0y, float (&e)[6]) {
+    e[0] = s[0];
+    e[1] = d0x * s[0] - s[1];
+    e[2] = d0y * s[0] - s[2];
+    e[3] = d0x * d0x * s[0] - 2.f * d0x * s[1] + s[3];
+    e[4] = d0x * d0y * s[0] - d0x * s[2] - d0y * s[1] + s[4];
+    e[5] = d0y * d0y * s[0] - 2.f * d0y * s[2] + s[5];
+}
+
 // DPP variant (cross-check of the MFMA default, R3DG_BWD=dpp): the reference's per-channel
 // recurrences (backward.cu:544-579) step by step; every wave reduces its 64 pixels' values of an
 // instance with DPP and lane 63 writes the wave's partial row.
@@ -93,6 +108,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
     float T = T_final;
     const float ddelx_dx = 0.5f * a.W, ddely_dy = 0.5f * a.H;
     const float xr = (float)(l & 7) - 3.5f, yr = (float)(l >> 3) - 3.5f;  // offset from the quadrant centre
+    const float qcx = (float)(tx * kTileX + (w & 1) * 8) + 3.5f, qcy = (float)(ty * kTileY + (w >> 1) * 8) + 3.5f;
 
     float acc[3] = {0.f, 0.f, 0.f}, acc_f[SMAX > 0 ? SMAX : 1], acc_d = 0.f, acc_o = 0.f;
     float last_alpha = 0.f, last_depth = 0.f, last_color[3] = {0.f, 0.f, 0.f}, last_f[SMAX > 0 ? SMAX : 1];
@@ -193,6 +209,10 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
                 const float sum = wave_sum_to_lane63(mv[k]);
                 if (l == 63) row[XW + k] = sum;
             }
+            if (l == 63) {
+                row[XW + 6] = qcx;
+                row[XW + 7] = qcy;
+            }
             if (l == 63) a.flags[(size_t)s_slot[j] * 4 + w] = 1;
         }
     }
@@ -243,13 +263,6 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
-#ifndef R3DG_BWD_YBF16
-#define R3DG_BWD_YBF16 1  // the moment (Y) products on the bf16 MFMA, q split into three bf16 terms
-#endif
-#ifndef R3DG_BWD_XBF16
-#define R3DG_BWD_XBF16 1  // the colour/feature/depth (X) products on the bf16 MFMA: w in three bf16
-                          // terms, the upstream gradients in two
-#endif
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // x = h + m + o to within 2^-24 |x|: three bf16 terms, each the round-to-nearest of what the
@@ -319,13 +332,9 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     float* wq = reinterpret_cast<float*>(s_lds + w * WQF4);
     int* s_max_last = reinterpret_cast<int*>(stage + 2 * SBUF);
 
-#if !R3DG_BWD_XBF16
-    float bX[NXB][16];
-#else
     // B operand of the X products (16x16x32 layout: lane l holds X[pixel 32b + 8(l >> 4) + i][channel
     // l & 15]) as two bf16 terms, X = hi + lo to within 2^-17 |X|
     bf16x8 bXh[NXB][2], bXl[NXB][2];
-#endif
     {
 #pragma unroll
         for (int xb = 0; xb < NXB; ++xb) {
@@ -339,10 +348,6 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 wq[c * WQS + l] = v;
             }
             wave_lds_sync();
-#if !R3DG_BWD_XBF16
-#pragma unroll
-            for (int s2 = 0; s2 < 16; ++s2) bX[xb][s2] = wq[(l & 15) * WQS + 4 * s2 + (l >> 4)];
-#else
 #pragma unroll
             for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -352,7 +357,6 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                     bXh[xb][b][i] = hb;
                     bXl[xb][b][i] = (__bf16)(x - (float)hb);
                 }
-#endif
             wave_lds_sync();
         }
     }
@@ -373,7 +377,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     }
     float u = 0.f;
     const float TFB = T_final * bg_dot;
-    int rowj = 0;
+    int rowj = 0;  // group row r's partial-row index (4 * slot + quadrant) in lane r
+    const float qcx = (float)(tx * kTileX + (w & 1) * 8) + 3.5f, qcy = (float)(ty * kTileY + (w >> 1) * 8) + 3.5f;
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
     const int max_last = block_max_last(wmax, s_max_last);
     const int RS = a.RS;
@@ -410,9 +415,9 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         u = __builtin_fmaf(ae, diff, u);
     };
 
-#if R3DG_BWD_YBF16
     // B operand of the moment products, constant: lane l holds Y[pixel 32b + 8(l >> 4) + i][l & 15]
-    // for K-block b (16x16x32 layout), pixel p = (p >> 3) * 8 + (p & 7) about the quadrant centre
+    // for K-block b (16x16x32 layout), pixel p = (p >> 3) * 8 + (p & 7) about the quadrant centre;
+    // exact in bf16 (at most 6 significant bits)
     bf16x8 yb[2];
 #pragma unroll
     for (int b = 0; b < 2; ++b)
@@ -422,58 +427,20 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             const float x = (float)(p & 7) - 3.5f, y = (float)(p >> 3) - 3.5f;
             const float v = nch == 0 ? 1.f : nch == 1 ? x : nch == 2 ? y : nch == 3 ? x * x : nch == 4 ? x * y
                           : nch == 5 ? y * y : 0.f;
-            yb[b][i] = (__bf16)v;  // exact: at most 6 significant bits
+            yb[b][i] = (__bf16)v;
         }
-#endif
+    // pad lanes of the moment stores: the quadrant centre (row_sum expands the moments about the mean)
+    const float cpad = nch == 6 ? qcx : qcy;
     auto flush = [&](int r) {
         if (l == 0) R3DG_EXP_ADD(1, 1);
 #ifdef R3DG_EXP_NOFLUSH  // timing experiment only (results invalid): no reduction, no rows
         (void)r;
         return;
 #endif
-#if !R3DG_BWD_YBF16
-        float yA[2], yB[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const float xo = (float)(4 * h + (l >> 4)) - 3.5f;
-            yA[h] = nch == 0 ? 1.f : (nch == 1 ? xo : (nch == 3 ? xo * xo : 0.f));
-            yB[h] = nch == 2 ? 1.f : (nch == 4 ? xo : 0.f);
-        }
-        const float yC = nch == 5 ? 1.f : 0.f;
-#endif
         wave_lds_sync();
         floatx4 accX[NXB], accY = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int xb = 0; xb < NXB; ++xb) accX[xb] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) {
-            const int col = 4 * s2 + (l >> 4);
-#if !R3DG_BWD_XBF16
-            const float av = wq[(l & 15) * WQS + col];
-#endif
-#if !R3DG_BWD_YBF16
-            const float aq = wq[(GRP + (l & 15)) * WQS + col];
-#endif
-#if !R3DG_BWD_XBF16
-#ifndef R3DG_EXP_NOXMFMA  // timing experiments only (results invalid): drop the X / Y products
-#pragma unroll
-            for (int xb = 0; xb < NXB; ++xb)
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bX[xb][s2], accX[xb], 0, 0, 0);
-#else
-            accX[0][s2 & 3] += av;
-#endif
-#endif
-#if !R3DG_BWD_YBF16
-            const float yo = (float)(s2 >> 1) - 3.5f;
-            const float by = yA[s2 & 1] + yo * (yB[s2 & 1] + yo * yC);
-#ifndef R3DG_EXP_NOYMFMA
-            accY = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, by, accY, 0, 0, 0);
-#else
-            accY[s2 & 3] += aq * by;
-#endif
-#endif
-        }
-#if R3DG_BWD_XBF16
         // w rows times the upstream gradients on the bf16 MFMA: w = w1 + w2 + w3 (three terms), X =
         // X1 + X2; the five products above 2^-24 of w X, smallest first
 #pragma unroll
@@ -493,8 +460,6 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
             }
         }
-#endif
-#if R3DG_BWD_YBF16
         // q rows times the moments on the bf16 MFMA (16 cycles per K = 32, against 32 per K = 4 in
         // f32): three exact-sum bf16 terms of q per K-block
 #pragma unroll
@@ -509,7 +474,6 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, yb[b], accY, 0, 0, 0);
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o, yb[b], accY, 0, 0, 0);
         }
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = (l >> 4) * 4 + i;
@@ -520,7 +484,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 float* dst = reinterpret_cast<float*>(reinterpret_cast<float4*>(a.rows) + base * (uint32_t)(RS >> 2));
 #pragma unroll
                 for (int xb = 0; xb < NXB; ++xb) dst[xb * 16 + nch] = accX[xb][i];
-                if (nch < 6) dst[XW + nch] = accY[i];
+                const float mv = nch < 6 ? accY[i] : cpad;
+                if (nch < 8) dst[XW + nch] = mv;
                 if (nch == 0) a.flags[base] = 1;
             }
         }
@@ -1019,11 +984,12 @@ hipError_t launch_sh_grad_views(int g0, int n, int deg, int M, int N, const floa
 // contiguous range 4 * [k0, k1) (row 4 * slot + quadrant); per chunk of 8 slots, lanes 0..7 load
 // one flag word each and the group ORs them into a 32-bit (slot, quadrant) presence mask, then
 // walks the present rows four at a time with independent loads (absent tail rows load nothing).
-// Lane c loads float4 column c of every row: c < NXC sums the X part; c == NXC expands
-// each row's quadrant-centred moments [S0, Sx, Sy, Sxx] about the Gaussian's mean (dx = mean.x -
-// pixel.x = d0x - x with d0x = mean.x - quadrant centre); c == NXC + 1 sums [Sxy, Syy], the
-// moments whose expansion needs no coefficient. Writes sums + g * RS = [X part (XW) | dL/dmean2D
-// x, y | dL/dconic x, y, z | dL/dopacity | 0, 0] (backward.cu:552-611 summed over the pixels).
+// Lane c sums float4 column c of every row (c < NXC: the X part); the two moment lanes NXC and
+// NXC + 1 swap their columns [S0, Sx, Sy, Sxx], [Sxy, Syy, cx, cy] (DPP) and expand each row's
+// moments about the Gaussian's mean with d0 = mean - (cx, cy) (expand_moments): lane NXC sums
+// [S0, Sdx, Sdy, Sdxdx], lane NXC + 1 [Sdxdy, Sdydy]. Writes sums + g * RS = [X part (XW) |
+// dL/dmean2D x, y | dL/dconic x, y, z | dL/dopacity | 0, 0] (backward.cu:552-611 summed over the
+// pixels).
 #ifndef R3DG_ROWSUM_PF
 #define R3DG_ROWSUM_PF 1  // row-sum: next chunk's flag word prefetched
 #endif
@@ -1040,19 +1006,14 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
     const int g = gb + (int)threadIdx.x / LPG, c = (int)threadIdx.x % LPG;
     const bool active = g < a.g_end && c < NXC + 2;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    float S0 = 0.f, Sdx = 0.f, Sdy = 0.f, Sdxdx = 0.f, Sdxdy = 0.f, Sdydy = 0.f;
     uint32_t k0 = 0, n = 0;
     float2 xy = make_float2(0.f, 0.f);
-    int x0 = 0, y0 = 0, rw = 1;
     if (g < a.g_end && a.rows && a.radii[g] > 0) {  // uniform within the group
         k0 = g == 0 ? 0u : a.offsets[g - 1];
         n = a.offsets[g] - k0;
         xy = a.means2D[g];
-        int x1, y1;
-        get_rect(xy.x, xy.y, a.radii[g], a.grid_x, a.grid_y, x0, y0, x1, y1);
-        rw = max(x1 - x0, 1);
     }
-    const float inv_rw = 1.f / (float)rw;
+    const bool mom = c >= NXC;                    // a moment lane (NXC, NXC + 1) or idle
 #if R3DG_ROWSUM_PF
     // the next chunk's flag word is loaded before this chunk's rows: one dependent round trip per
     // chunk instead of two
@@ -1072,49 +1033,48 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
         for (int o = 1; o < LPG; o <<= 1) mask |= __shfl_xor(mask, o);
         const float* base = a.rows + (size_t)(k0 + kb) * 4 * RS;
         while (mask) {
-            int bit[4];
             float4 v[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                bit[i] = mask ? __builtin_ctz(mask) : 0;
+                const int bit = mask ? __builtin_ctz(mask) : 0;
                 const bool has = mask != 0u;
-                const float* row = base + (size_t)bit[i] * RS;
+                const float4* row = reinterpret_cast<const float4*>(base + (size_t)bit * RS);
                 mask &= mask - 1u;
-                v[i] = active && has ? reinterpret_cast<const float4*>(row)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+                v[i] = active && has ? row[c] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            if (c < NXC || c == NXC + 1) {
+            if (!mom) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
                 }
-            } else if (c == NXC) {
+            } else {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    // tile of slot kb + bit/4 in the row-major rect (slot order = duplicateWithKeys)
-                    const int idx = (int)kb + (bit[i] >> 2), q = bit[i] & 3;
-                    const int iy = (int)(((float)idx + 0.5f) * inv_rw), ix = idx - iy * rw;
-                    const float4 m = v[i];  // S0 Sx Sy Sxx (zero for an absent row)
-                    const float d0x = xy.x - ((float)((x0 + ix) * kTileX + (q & 1) * 8) + 3.5f);
-                    const float d0y = xy.y - ((float)((y0 + iy) * kTileY + (q >> 1) * 8) + 3.5f);
-                    S0 += m.x;
-                    Sdx += d0x * m.x - m.y;
-                    Sdy += d0y * m.x - m.z;
-                    Sdxdx += d0x * d0x * m.x - 2.f * d0x * m.y + m.w;
-                    Sdxdy += d0x * d0y * m.x - d0x * m.z - d0y * m.y;
-                    Sdydy += d0y * d0y * m.x - 2.f * d0y * m.z;
+                    // the other moment column from the neighbouring lane (DPP quad_perm [1, 0, 3, 2])
+                    const float4 vo = make_float4(dpp_mov<0xB1>(v[i].x), dpp_mov<0xB1>(v[i].y), dpp_mov<0xB1>(v[i].z),
+                                                  dpp_mov<0xB1>(v[i].w));
+                    const float4 m0 = c == NXC ? v[i] : vo, m1 = c == NXC ? vo : v[i];
+                    const float sm[6] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y};
+                    float e[6];
+                    // an absent row is all zero: its centre (0, 0) multiplies zero moments
+                    expand_moments(sm, xy.x - m1.z, xy.y - m1.w, e);
+                    if (c == NXC) {
+                        acc.x += e[0]; acc.y += e[1]; acc.z += e[2]; acc.w += e[3];
+                    } else {
+                        acc.x += e[4]; acc.y += e[5];
+                    }
                 }
             }
         }
     }
-    // lane NXC takes the [Sxy, Syy] sums of lane NXC + 1 (all lanes take part in the shuffle)
+    // lane NXC takes the [Sdxdy, Sdydy] sums of lane NXC + 1 (all lanes take part in the shuffle)
     const float sxy = __shfl_down(acc.x, 1), syy = __shfl_down(acc.y, 1);
     if (!active) return;
     float4* dst = reinterpret_cast<float4*>(a.sums + (size_t)g * RS);
     if (c < NXC) {
         dst[c] = acc;
     } else if (c == NXC) {
-        Sdxdy += sxy;
-        Sdydy += syy;
+        const float S0 = acc.x, Sdx = acc.y, Sdy = acc.z, Sdxdx = acc.w, Sdxdy = sxy, Sdydy = syy;
         const float4 co = a.conic_opacity[g];
         // dL/dmean2D = -0.5 (W, H) o (o * conic . (Sdx, Sdy)), dL/dconic = -0.5 o (Sdxdx, Sdxdy,
         // Sdydy), dL/dopacity = S0 (backward.cu:583-611)
