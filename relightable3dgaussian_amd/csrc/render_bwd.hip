@@ -486,7 +486,6 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 for (int xb = 0; xb < NXB; ++xb) dst[xb * 16 + nch] = accX[xb][i];
                 const float mv = nch < 6 ? accY[i] : cpad;
                 if (nch < 8) dst[XW + nch] = mv;
-                if (nch == 0) a.flags[base] = 1;
             }
         }
         wave_lds_sync();
@@ -549,13 +548,19 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         st = stage + buf * SBUF;
         // this wave's live instances: the forward's contribution bits for its quadrant (lanes
         // 0..cnt-1; zero past the batch)
-        uint32_t slot_l = 0u;
+        // this wave's partial row of instance l (4 * slot + quadrant), flagged here, once per
+        // visited instance (rather than by the flush's row stores)
+        uint32_t row_l = 0u;
         const bool mine = (cbits >> w) & 1u;
-        if (mine) slot_l = record_slot(st[NB + l], tx, ty, a.grid_x, a.grid_y);
         mask_t bits = (mask_t)__ballot(mine);
         const int lo = hi - wmax;  // instances j < lo lie beyond every pixel of this wave
         if (lo >= NB) bits = 0u;
         else if (lo > 0) bits &= ~(mask_t)0 << lo;
+        if ((bits >> l) & 1u) {
+            const uint32_t slot = record_slot(st[NB + l], tx, ty, a.grid_x, a.grid_y);
+            row_l = 4 * slot + w;
+            a.flags[row_l] = 1;
+        }
 #ifdef R3DG_EXP_COUNT
         if (l == 0) R3DG_EXP_ADD(0, __builtin_popcountll(bits));
         t_mask += wall_clock64() - tm0;
@@ -597,13 +602,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 float* wr = wq + r * WQS + l;
                 wr[0] = wv0;
                 wr[GRP * WQS] = qv0;
-                rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j0) * 4 + w), r);
+                rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j0), r);
             }
             if (has1) {
                 float* wr = wq + (r + 1) * WQS + l;
                 wr[0] = wv1;
                 wr[GRP * WQS] = qv1;
-                rowj = write_lane(rowj, (int)(__builtin_amdgcn_readlane(slot_l, j1) * 4 + w), r + 1);
+                rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j1), r + 1);
             }
             r += has1 ? 2 : 1;
             if (r > GRP - 2) {
