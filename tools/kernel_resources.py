@@ -9,7 +9,7 @@ import tempfile
 import yaml
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-obj = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "relightable3dgaussian_amd", "build", "obj",
+obj = os.path.join(os.environ.get("R3DG_OBJ_DIR") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "relightable3dgaussian_amd", "build", "obj"),
                    sys.argv[1] + ".o")
 pat = re.compile(sys.argv[2] if len(sys.argv) > 2 else ".")
 with tempfile.TemporaryDirectory() as d:
