@@ -171,10 +171,10 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
         for (int i = idx; i < a.num_tiles; i += (int)(gridDim.x * 256)) a.tile_count[i] = 0u;
     if (use_sh) {
         const float* src = a.sh + (size_t)g0 * M3;
-        for (int f = t; f < ng * M3; f += 256) {
+        block_load4<256>(src, ng * M3, t, [&](int f, float v) {
             const int gg = f / M3;
-            s_buf[gg * SHS + (f - gg * M3)] = src[f];
-        }
+            s_buf[gg * SHS + (f - gg * M3)] = v;
+        });
     }
     __syncthreads();
     float4 rec0, rec1;

@@ -164,6 +164,43 @@ __device__ __forceinline__ float wave_sum_to_lane63(float v) {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Copies of a workgroup's contiguous span of n floats (float4 accesses when 16-byte aligned) between global memory and
+// an LDS layout: float4 global accesses, kCopyU of them in flight per thread before the LDS side
+// (the per-Gaussian kernels' SH staging; one dword per access kept 8 loads in flight). put(f, v) /
+// get(f) map element f to its LDS slot.
+constexpr int kCopyU = 6;
+template <int BT, class F>
+__device__ __forceinline__ void block_load4(const float* __restrict__ src, int n, int t, F&& put) {
+    const int n4 = (reinterpret_cast<uintptr_t>(src) & 15u) ? 0 : n >> 2;  // unaligned: dword copies
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    for (int b = t; b < n4; b += BT * kCopyU) {
+        float4 v[kCopyU];
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const int i = b + u * BT;
+            v[u] = i < n4 ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const int i = b + u * BT;
+            if (i < n4) {
+                put(4 * i, v[u].x);
+                put(4 * i + 1, v[u].y);
+                put(4 * i + 2, v[u].z);
+                put(4 * i + 3, v[u].w);
+            }
+        }
+    }
+    for (int f = 4 * n4 + t; f < n; f += BT) put(f, src[f]);
+}
+template <int BT, class F>
+__device__ __forceinline__ void block_store4(float* __restrict__ dst, int n, int t, F&& get) {
+    const int n4 = (reinterpret_cast<uintptr_t>(dst) & 15u) ? 0 : n >> 2;  // unaligned: dword copies
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (int i = t; i < n4; i += BT) d4[i] = make_float4(get(4 * i), get(4 * i + 1), get(4 * i + 2), get(4 * i + 3));
+    for (int f = 4 * n4 + t; f < n; f += BT) dst[f] = get(f);
+}
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));  // MFMA accumulator fragment
 typedef float f32x2 __attribute__((ext_vector_type(2)));    // packed fp32 pair (v_pk_* ops)
 

@@ -1136,20 +1136,20 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     float* shl = s_buf + t * SHS;
     if (a.sh && a.dL_dsh) {
         const float* src = a.sh + (size_t)g0 * M3;
-        for (int f = t; f < ng * M3; f += 256) {
+        block_load4<256>(src, ng * M3, t, [&](int f, float v) {
             const int gg = f / M3;
-            s_buf[gg * SHS + (f - gg * M3)] = src[f];
-        }
+            s_buf[gg * SHS + (f - gg * M3)] = v;
+        });
     }
     __syncthreads();
     if (g < a.g_end) gather_gaussian<SMAX>(a, g, s, shl);
     __syncthreads();
     if (a.dL_dsh) {
         float* dst = a.dL_dsh + (size_t)g0 * M3;
-        for (int f = t; f < ng * M3; f += 256) {
+        block_store4<256>(dst, ng * M3, t, [&](int f) {
             const int gg = f / M3;
-            dst[f] = s_buf[gg * SHS + (f - gg * M3)];
-        }
+            return s_buf[gg * SHS + (f - gg * M3)];
+        });
     }
 }
 
