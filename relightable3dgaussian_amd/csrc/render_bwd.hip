@@ -995,6 +995,10 @@ hipError_t launch_sh_grad_views(int g0, int n, int deg, int M, int N, const floa
 // [S0, Sdx, Sdy, Sdxdx], lane NXC + 1 [Sdxdy, Sdydy]. Writes sums + g * RS = [X part (XW) |
 // dL/dmean2D x, y | dL/dconic x, y, z | dL/dopacity | 0, 0] (backward.cu:552-611 summed over the
 // pixels).
+#ifndef R3DG_ROWSUM_RPI
+#define R3DG_ROWSUM_RPI 4  // present rows loaded per iteration (independent float4 loads per lane;
+                           // measured at M1: 2 -> 0.230, 4 -> 0.206, 8 -> 0.215 ms)
+#endif
 #ifndef R3DG_ROWSUM_PF
 #define R3DG_ROWSUM_PF 1  // row-sum: next chunk's flag word prefetched
 #endif
@@ -1038,9 +1042,9 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
         for (int o = 1; o < LPG; o <<= 1) mask |= __shfl_xor(mask, o);
         const float* base = a.rows + (size_t)(k0 + kb) * 4 * RS;
         while (mask) {
-            float4 v[4];
+            float4 v[R3DG_ROWSUM_RPI];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < R3DG_ROWSUM_RPI; ++i) {
                 const int bit = mask ? __builtin_ctz(mask) : 0;
                 const bool has = mask != 0u;
                 const float4* row = reinterpret_cast<const float4*>(base + (size_t)bit * RS);
@@ -1049,12 +1053,12 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
             }
             if (!mom) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
+                for (int i = 0; i < R3DG_ROWSUM_RPI; ++i) {
                     acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
                 }
             } else {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
+                for (int i = 0; i < R3DG_ROWSUM_RPI; ++i) {
                     // the other moment column from the neighbouring lane (DPP quad_perm [1, 0, 3, 2])
                     const float4 vo = make_float4(dpp_mov<0xB1>(v[i].x), dpp_mov<0xB1>(v[i].y), dpp_mov<0xB1>(v[i].z),
                                                   dpp_mov<0xB1>(v[i].w));
