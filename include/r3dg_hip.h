@@ -114,6 +114,17 @@ int r3dg_rasterize_gaussians(const r3dg_raster_settings* settings, const r3dg_ga
                              r3dg_alloc_fn binning_alloc, void* binning_ctx, r3dg_alloc_fn image_alloc,
                              void* image_ctx, int* num_rendered, r3dg_stream_t stream);
 
+/* r3dg_rasterize_gaussians with a scratch allocator: the binning's per-workgroup tile counts
+ * (up to 8 MiB, [workgroups, tiles] u32, used only until the instances are scattered) come from
+ * scratch_alloc, which may hand out stream-ordered memory the caller frees as soon as the call
+ * returns (the torch binding passes the caching allocator), instead of the tail of the image
+ * state, which lives as long as the autograd context. scratch_alloc NULL = r3dg_rasterize_gaussians. */
+int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* settings, const r3dg_gaussians* g,
+                                const r3dg_forward_outputs* out, r3dg_alloc_fn geom_alloc, void* geom_ctx,
+                                r3dg_alloc_fn binning_alloc, void* binning_ctx, r3dg_alloc_fn image_alloc,
+                                void* image_ctx, r3dg_alloc_fn scratch_alloc, void* scratch_ctx, int* num_rendered,
+                                r3dg_stream_t stream);
+
 size_t r3dg_image_state_n_contrib_offset(int H, int W);
 
 /* Bytes of the geometry state buffer for P Gaussians with S features (S < 0: the S-independent
@@ -317,6 +328,14 @@ typedef struct r3dg_param_layout {
 int r3dg_adam_step(const r3dg_param_layout* layout, float* param, const float* grad, float* exp_avg,
                    float* exp_avg_sq, int64_t lo, int64_t hi, const float* lr_host, double beta1, double beta2,
                    double eps, int step, r3dg_stream_t stream);
+
+/* r3dg_adam_step with one Adam step count per group (torch keeps `state['step']` per parameter):
+ * steps_host[g] is group g's 1-based count for this step, or <= 0 when the group has no gradient
+ * this iteration -- torch.optim.Adam skips a parameter whose .grad is None (gaussian_model.py:615-617
+ * zero_grad(set_to_none=True)), so its param, exp_avg and exp_avg_sq stay untouched. */
+int r3dg_adam_step_groups(const r3dg_param_layout* layout, float* param, const float* grad, float* exp_avg,
+                          float* exp_avg_sq, int64_t lo, int64_t hi, const float* lr_host, const int* steps_host,
+                          double beta1, double beta2, double eps, r3dg_stream_t stream);
 
 /* train.py:172-176 + add_densification_stats (gaussian_model.py:1055-1062) for the Gaussians
  * with radii > 0 (visibility_filter): max_radii2D = max(max_radii2D, radii); xyz_accum +=

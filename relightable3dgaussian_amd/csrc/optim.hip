@@ -37,19 +37,23 @@ struct AdamArgs {
     long long lo, hi;
     int nseg;
     long long seg_end[R3DG_MAX_GROUPS];   // global end of each group
-    float neg_step[R3DG_MAX_GROUPS];      // -(lr / (1 - b1^t))
-    float bc2_sqrt;                       // sqrt(1 - b2^t): torch divides sqrt(v) by it
+    float neg_step[R3DG_MAX_GROUPS];      // -(lr / (1 - b1^t)); t = the group's own step count
+    float bc2_sqrt[R3DG_MAX_GROUPS];      // sqrt(1 - b2^t): torch divides sqrt(v) by it
+    unsigned skip;                        // bit g: group g has no gradient this step (grad None)
     float omb1, beta2, omb2, eps;
 };
 
-__device__ __forceinline__ float adam_elem(const AdamArgs& a, float p, float g, float& m, float& v, float ns) {
+__device__ __forceinline__ float adam_elem(const AdamArgs& a, float p, float g, float& m, float& v, float ns,
+                                           float bc2_sqrt, bool skip) {
+    // torch.optim.Adam leaves a parameter whose .grad is None untouched (p, m, v and its step)
+    if (skip) return p;
     // torch._foreach_lerp_(exp_avgs, grads, 1 - beta1): weight < 0.5 -> self + w * (end - self)
     m = __builtin_fmaf(a.omb1, g - m, m);
     // _foreach_mul_(exp_avg_sqs, beta2); _foreach_addcmul_(exp_avg_sqs, grads, grads, 1 - beta2)
     v = v * a.beta2;
     v = __builtin_fmaf(a.omb2, g * g, v);
     // denom = sqrt(v) / bias_correction2_sqrt + eps; param += step_size * m / denom
-    const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+    const float denom = sqrtf(v) / bc2_sqrt + a.eps;
     return __builtin_fmaf(ns, m / denom, p);
 }
 
@@ -59,12 +63,15 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
     if (i4 >= n) return;
     const long long gi = a.lo + i4;
     // group of each of the 4 floats (segments are few; a float4 may straddle a boundary)
-    float ns[4];
+    float ns[4], bc[4];
+    bool sk[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         int s = 0;
         while (s < a.nseg - 1 && gi + e >= a.seg_end[s]) ++s;
         ns[e] = a.neg_step[s];
+        bc[e] = a.bc2_sqrt[s];
+        sk[e] = (a.skip >> s) & 1u;
     }
     const bool vec = i4 + 4 <= n && (((uintptr_t)(a.param + gi) | (uintptr_t)(a.grad + i4) |
                                       (uintptr_t)(a.m + i4) | (uintptr_t)(a.v + i4)) & 15) == 0;
@@ -73,17 +80,17 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
         const float4 g = *reinterpret_cast<const float4*>(a.grad + i4);
         float4 m = *reinterpret_cast<const float4*>(a.m + i4);
         float4 v = *reinterpret_cast<const float4*>(a.v + i4);
-        p.x = adam_elem(a, p.x, g.x, m.x, v.x, ns[0]);
-        p.y = adam_elem(a, p.y, g.y, m.y, v.y, ns[1]);
-        p.z = adam_elem(a, p.z, g.z, m.z, v.z, ns[2]);
-        p.w = adam_elem(a, p.w, g.w, m.w, v.w, ns[3]);
+        p.x = adam_elem(a, p.x, g.x, m.x, v.x, ns[0], bc[0], sk[0]);
+        p.y = adam_elem(a, p.y, g.y, m.y, v.y, ns[1], bc[1], sk[1]);
+        p.z = adam_elem(a, p.z, g.z, m.z, v.z, ns[2], bc[2], sk[2]);
+        p.w = adam_elem(a, p.w, g.w, m.w, v.w, ns[3], bc[3], sk[3]);
         *reinterpret_cast<float4*>(a.param + gi) = p;
         *reinterpret_cast<float4*>(a.m + i4) = m;
         *reinterpret_cast<float4*>(a.v + i4) = v;
     } else {
         for (int e = 0; e < 4 && i4 + e < n; ++e) {
             float m = a.m[i4 + e], v = a.v[i4 + e];
-            a.param[gi + e] = adam_elem(a, a.param[gi + e], a.grad[i4 + e], m, v, ns[e]);
+            a.param[gi + e] = adam_elem(a, a.param[gi + e], a.grad[i4 + e], m, v, ns[e], bc[e], sk[e]);
             a.m[i4 + e] = m;
             a.v[i4 + e] = v;
         }
@@ -280,31 +287,52 @@ __global__ void __launch_bounds__(256) reset_opacity_kernel(int P, float* op, fl
 
 using namespace r3dg;
 
-extern "C" int r3dg_adam_step(const r3dg_param_layout* L, float* param, const float* grad, float* exp_avg,
-                              float* exp_avg_sq, int64_t lo, int64_t hi, const float* lr_host, double beta1,
-                              double beta2, double eps, int step, r3dg_stream_t stream) {
+extern "C" int r3dg_adam_step_groups(const r3dg_param_layout* L, float* param, const float* grad, float* exp_avg,
+                                     float* exp_avg_sq, int64_t lo, int64_t hi, const float* lr_host,
+                                     const int* steps_host, double beta1, double beta2, double eps,
+                                     r3dg_stream_t stream) {
     if (int e = check_layout(L)) return e;
     const long long total = (long long)L->P * layout_width(L);
     R3DG_REQUIRE(0 <= lo && lo <= hi && hi <= total, "adam_step: shard [lo, hi) outside the parameter buffer");
-    R3DG_REQUIRE(step >= 1 && lr_host, "adam_step: step must be >= 1 and lr given");
+    R3DG_REQUIRE(lr_host && steps_host, "adam_step: lr and steps given");
     if (hi == lo) return R3DG_OK;
     R3DG_REQUIRE(param && grad && exp_avg && exp_avg_sq, "adam_step: null buffer");
     AdamArgs a{};
     a.param = param; a.grad = grad; a.m = exp_avg; a.v = exp_avg_sq; a.lo = lo; a.hi = hi;
     a.nseg = L->n_groups;
     long long end = 0;
-    const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
+    bool any = false;
     for (int g = 0; g < L->n_groups; ++g) {
         end += (long long)L->P * L->width[g];
         a.seg_end[g] = end;
+        const int t = steps_host[g];
+        if (t <= 0) {
+            a.skip |= 1u << g;
+            a.bc2_sqrt[g] = 1.f;
+            continue;
+        }
+        any = true;
+        const double bc1 = 1.0 - std::pow(beta1, (double)t), bc2 = 1.0 - std::pow(beta2, (double)t);
         a.neg_step[g] = (float)(-((double)lr_host[g] / bc1));
+        a.bc2_sqrt[g] = (float)std::sqrt(bc2);
     }
-    a.bc2_sqrt = (float)std::sqrt(bc2);
+    if (!any) return R3DG_OK;
     a.omb1 = (float)(1.0 - beta1); a.beta2 = (float)beta2; a.omb2 = (float)(1.0 - beta2); a.eps = (float)eps;
     const long long n4 = (hi - lo + 3) / 4;
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
     R3DG_CHECK_HIP(hipGetLastError());
     return R3DG_OK;
+}
+
+extern "C" int r3dg_adam_step(const r3dg_param_layout* L, float* param, const float* grad, float* exp_avg,
+                              float* exp_avg_sq, int64_t lo, int64_t hi, const float* lr_host, double beta1,
+                              double beta2, double eps, int step, r3dg_stream_t stream) {
+    if (int e = check_layout(L)) return e;
+    R3DG_REQUIRE(step >= 1 && lr_host, "adam_step: step must be >= 1 and lr given");
+    int steps[R3DG_MAX_GROUPS];
+    for (int g = 0; g < L->n_groups; ++g) steps[g] = step;
+    return r3dg_adam_step_groups(L, param, grad, exp_avg, exp_avg_sq, lo, hi, lr_host, steps, beta1, beta2, eps,
+                                 stream);
 }
 
 extern "C" int r3dg_densification_stats(int P, const float* dL_dmeans2D, int stride2d, const float* normal_grad,

@@ -87,7 +87,7 @@ struct ImageState {
 
 size_t geom_state_bytes(size_t P, int S);
 size_t binning_state_bytes(size_t L);
-size_t image_state_bytes(int H, int W);
+size_t image_state_bytes(int H, int W, bool with_hist = true);
 GeomState geom_state_from(void* base, size_t P, int S = -1);
 BinningState binning_state_from(void* base, size_t L);
 ImageState image_state_from(void* base, int H, int W);

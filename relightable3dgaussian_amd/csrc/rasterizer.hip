@@ -119,8 +119,9 @@ size_t binning_state_bytes(size_t L) {
 BinningState binning_state_from(void* base, size_t L) { return carve_binning((uintptr_t)base, L, nullptr); }
 
 static int num_tiles_of(int H, int W) { return ((W + kTileX - 1) / kTileX) * ((H + kTileY - 1) / kTileY); }
+static size_t bin_hist_count(size_t T) { return (size_t)bin_blocks_max((int)T) * T; }
 
-static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end) {
+static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end, bool with_hist = true) {
     ImageState s{};
     const size_t N = (size_t)H * W;
     s.final_T = carve<float>(p, N);
@@ -129,16 +130,20 @@ static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end) {
     s.ranges = carve<uint2>(p, T);
     s.tile_order = carve<uint32_t>(p, T);
     s.tile_work = carve<uint32_t>(p, T);
-    s.bin_hist = carve<uint32_t>(p, (size_t)bin_blocks_max((int)T) * T);
+    // the binning's per-workgroup tile counts: last, so the backward's view of the buffer does
+    // not depend on whether they live here (r3dg_rasterize_gaussians) or in transient scratch
+    // (r3dg_rasterize_gaussians_ex)
+    if (with_hist) s.bin_hist = carve<uint32_t>(p, bin_hist_count(T));
     if (end) *end = p;
     return s;
 }
-size_t image_state_bytes(int H, int W) {
+size_t image_state_bytes(int H, int W, bool with_hist) {
     uintptr_t end = 0;
-    carve_image(0, H, W, &end);
+    carve_image(0, H, W, &end, with_hist);
     return (size_t)end;
 }
-ImageState image_state_from(void* base, int H, int W) { return carve_image((uintptr_t)base, H, W, nullptr); }
+// the backward and the accessors never read the tile counts
+ImageState image_state_from(void* base, int H, int W) { return carve_image((uintptr_t)base, H, W, nullptr, false); }
 
 // ---- profiling events (r3dg_profile_*) -----------------------------------------------------------
 struct Profiler {
@@ -359,6 +364,15 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
                                         const r3dg_forward_outputs* out, r3dg_alloc_fn geom_alloc, void* geom_ctx,
                                         r3dg_alloc_fn binning_alloc, void* binning_ctx, r3dg_alloc_fn image_alloc,
                                         void* image_ctx, int* num_rendered, r3dg_stream_t stream) {
+    return r3dg_rasterize_gaussians_ex(s, g, out, geom_alloc, geom_ctx, binning_alloc, binning_ctx, image_alloc,
+                                       image_ctx, nullptr, nullptr, num_rendered, stream);
+}
+
+extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const r3dg_gaussians* g,
+                                           const r3dg_forward_outputs* out, r3dg_alloc_fn geom_alloc, void* geom_ctx,
+                                           r3dg_alloc_fn binning_alloc, void* binning_ctx, r3dg_alloc_fn image_alloc,
+                                           void* image_ctx, r3dg_alloc_fn scratch_alloc, void* scratch_ctx,
+                                           int* num_rendered, r3dg_stream_t stream) {
     hipStream_t st = (hipStream_t)stream;
     R3DG_REQUIRE(s && g && out && num_rendered, "rasterize_gaussians: null argument");
     const int P = s->P, S = s->S, H = s->H, W = s->W;
@@ -463,13 +477,18 @@ extern "C" int r3dg_rasterize_gaussians(const r3dg_raster_settings* s, const r3d
     const size_t work_floats = work_copies ? (size_t)P * (3 + 3 + 4 + 1 + M3 + S) : 0;
     const size_t post_floats = post_blur ? (size_t)3 * H * W : 0;  // BlurLighting's incident-light snapshot
     void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * (work_floats + post_floats));
-    void* img_base = image_alloc(image_ctx, image_state_bytes(H, W));
-    if (!geom_base || !img_base) {
+    // with a scratch allocator the binning's tile counts are transient (needed only until the
+    // scatter), not part of the image state autograd keeps alive until the backward
+    const bool hist_scratch = scratch_alloc != nullptr && P > 0;
+    void* img_base = image_alloc(image_ctx, image_state_bytes(H, W, !hist_scratch));
+    uint32_t* hist_base = hist_scratch ? (uint32_t*)scratch_alloc(scratch_ctx, 4 * bin_hist_count((size_t)T)) : nullptr;
+    if (!geom_base || !img_base || (hist_scratch && !hist_base)) {
         set_error("rasterize_gaussians: state allocation failed");
         return R3DG_ERR_ALLOC;
     }
     GeomState geom = geom_state_from(geom_base, (size_t)P, S);
-    ImageState img = image_state_from(img_base, H, W);
+    ImageState img = carve_image((uintptr_t)img_base, H, W, nullptr, !hist_scratch);
+    if (hist_scratch) img.bin_hist = hist_base;
     int* radii = out->radii ? out->radii : geom.internal_radii;
     const float focal_y = H / (2.0f * s->tan_fovy);
     const float focal_x = W / (2.0f * s->tan_fovx);

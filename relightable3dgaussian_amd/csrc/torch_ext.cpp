@@ -125,8 +125,10 @@ FwdResult rasterize_gaussians(const torch::Tensor& background, double time, doub
     o.normal = out_normal.data_ptr<float>(); o.surface_xyz = out_xyz.data_ptr<float>();
     o.radii = P > 0 ? radii.data_ptr<int>() : nullptr;
     int rendered = 0;
-    check(r3dg_rasterize_gaussians(&s, &g, &o, tensor_alloc, &ga, tensor_alloc, &ba, tensor_alloc, &ia, &rendered,
-                                   stream_of(dev)),
+    // the binning's tile counts: transient, returned to the caching allocator (stream-ordered) on exit
+    TensorAlloc hist{bopt, torch::empty({0}, bopt)};
+    check(r3dg_rasterize_gaussians_ex(&s, &g, &o, tensor_alloc, &ga, tensor_alloc, &ba, tensor_alloc, &ia, tensor_alloc,
+                                      &hist, &rendered, stream_of(dev)),
           "rasterize_gaussians");
     // n_contrib is a view into the image state buffer (reference: from_blob, rasterize_points.cu:179)
     const int64_t off = (int64_t)r3dg_image_state_n_contrib_offset(H, W);
@@ -613,6 +615,25 @@ void adam_step(int64_t P, const std::vector<int64_t>& widths, const std::vector<
           "adam_step");
 }
 
+// adam_step with one step count per group; steps[g] <= 0: group g has no gradient (skipped)
+void adam_step_groups(int64_t P, const std::vector<int64_t>& widths, const std::vector<int64_t>& roles,
+                      torch::Tensor param, const torch::Tensor& grad, torch::Tensor exp_avg, torch::Tensor exp_avg_sq,
+                      int64_t lo, int64_t hi, const std::vector<double>& lrs, double beta1, double beta2, double eps,
+                      const std::vector<int64_t>& steps) {
+    const r3dg_param_layout L = make_layout(P, widths, roles);
+    TORCH_CHECK(lrs.size() == widths.size() && steps.size() == widths.size(),
+                "adam_step_groups: one learning rate and one step count per group");
+    TORCH_CHECK(grad.numel() == hi - lo && exp_avg.numel() == hi - lo && exp_avg_sq.numel() == hi - lo,
+                "adam_step_groups: grad / exp_avg / exp_avg_sq must hold the shard's hi - lo floats");
+    const c10::OptionalDeviceGuard guard(param.device());
+    std::vector<float> lr(lrs.begin(), lrs.end());
+    std::vector<int> st(steps.begin(), steps.end());
+    check(r3dg_adam_step_groups(&L, f32_ptr(param, "param"), f32_ptr(grad, "grad"), f32_ptr(exp_avg, "exp_avg"),
+                                f32_ptr(exp_avg_sq, "exp_avg_sq"), lo, hi, lr.data(), st.data(), beta1, beta2, eps,
+                                stream_of(param.device())),
+          "adam_step_groups");
+}
+
 void densification_stats(const torch::Tensor& dL_dmeans2D, const torch::Tensor& normal_grad, const torch::Tensor& radii,
                          torch::Tensor xyz_accum, torch::Tensor normal_accum, torch::Tensor denom,
                          torch::Tensor max_radii2D) {
@@ -859,6 +880,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("abi_version", []() { return r3dg_abi_version(); });
     // training step on the device (§8f rank 3)
     m.def("adam_step", &adam_step);
+    m.def("adam_step_groups", &adam_step_groups);
     m.def("densification_stats", &densification_stats);
     m.def("densify_and_prune", &densify_and_prune);
     m.def("reset_opacity", &reset_opacity);

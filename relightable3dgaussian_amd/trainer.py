@@ -206,17 +206,33 @@ class GaussianTrainState:
         self.lrs[[n for n, _ in self.groups].index("xyz")] = float(lr)
         return lr
 
-    def step(self, adam_fn=None, zero_grad: bool = False):
+    def step(self, adam_fn=None, zero_grad: bool = True, absent=()):
         """optimizer.step() + zero_grad(set_to_none=True) (gaussian_model.py:615-617); sharded over
-        ranks. As with the reference's set-to-None gradients, the next step's gradients are written
-        (grad_view(name).copy_ / the backward's outputs), not accumulated, so the buffer is not
-        cleared; pass zero_grad=True when the caller accumulates into it."""
+        ranks. `absent` names the groups whose gradient is None this iteration: torch.optim.Adam
+        skips them (param, exp_avg, exp_avg_sq and the group's step count stay as they are), so
+        they are skipped here too (per-group step counts, `_C.adam_step_groups`). The gradient
+        buffer is cleared after the step (zero_grad=True, the default), so a group the caller does
+        not write before the next step contributes a zero gradient, never the previous one; pass
+        zero_grad=False only when every group is rewritten each step."""
         import torch.distributed as dist
 
         from . import _C
 
-        adam = adam_fn or _C.adam_step
+        names = [n for n, _ in self.groups]
+        bad = set(absent) - set(names)
+        if bad:
+            raise KeyError(f"step: unknown groups {sorted(bad)}")
+        gs = getattr(self, "group_steps", None)
+        if gs is None or len(gs) != len(names):
+            gs = self.group_steps = [self.step_count] * len(names)
         self.step_count += 1
+        steps = []
+        for i, n in enumerate(names):
+            if n in absent:
+                steps.append(0)
+            else:
+                gs[i] += 1
+                steps.append(gs[i])
         lo, hi = self.shard_range()
         s = self.shard_size()
         if self.dist.world > 1:
@@ -225,9 +241,15 @@ class GaussianTrainState:
             g = g[:hi - lo]
         else:
             g = self.grad[lo:hi]
-        adam(self.P, self.widths(), self.roles(), self.param, g.contiguous(), self.exp_avg[:hi - lo],
-             self.exp_avg_sq[:hi - lo], lo, hi, list(self.lrs), self.betas[0], self.betas[1], self.eps,
-             self.step_count)
+        args = (self.P, self.widths(), self.roles(), self.param, g.contiguous(), self.exp_avg[:hi - lo],
+                self.exp_avg_sq[:hi - lo], lo, hi, list(self.lrs), self.betas[0], self.betas[1], self.eps)
+        uniform = len(set(steps)) == 1 and steps[0] > 0
+        if adam_fn is not None:
+            adam_fn(*args, steps[0] if uniform else steps)
+        elif uniform:
+            _C.adam_step(*args, steps[0])
+        else:
+            _C.adam_step_groups(*args, steps)
         if self.dist.world > 1:
             dist.all_gather_into_tensor(self.param, self.param[self.dist.rank * s:(self.dist.rank + 1) * s].clone(),
                                         group=self.dist.group)

@@ -258,3 +258,83 @@ def test_gpu_prune_only_and_adam_large(hip_ext):
     assert 0 < st.P == int(keep_ref.sum()) < P
     np.testing.assert_array_equal(st.view("xyz").cpu().numpy(), xyz_before[keep_ref])
     assert float(st.denom.min()) == 3.0  # survivors keep their statistics
+
+
+def _cpu_adam_groups(P, widths, roles, param, g, m, v, lo, hi, lrs, b1, b2, eps, steps):
+    """Per-group oracle Adam: steps is one int (all groups) or one count per group, <= 0 = skip."""
+    import torch
+
+    steps = [steps] * len(widths) if np.isscalar(steps) else list(steps)
+    bounds = np.cumsum([0] + [P * w for w in widths])
+    for gi_, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
+        a, b = max(a, lo), min(b, hi)
+        if a >= b or steps[gi_] <= 0:
+            continue
+        sl = slice(a - lo, b - lo)
+        p, mm, vv = T.adam_step(param[a:b].numpy(), g[sl].numpy(), m[sl].numpy(), v[sl].numpy(), lrs[gi_],
+                                steps[gi_], b1, b2, eps)
+        param[a:b] = torch.from_numpy(p)
+        m[sl] = torch.from_numpy(mm)
+        v[sl] = torch.from_numpy(vv)
+
+
+def _absent_sequence(st, adam_fn, dev):
+    """Three steps; "normal" has no gradient in step 1 (grad None in the reference) and "opacity"
+    is simply not written in step 2. Returns the per-step snapshots of both groups."""
+    import torch
+
+    rng = np.random.default_rng(7)
+    snaps = []
+    for k in range(3):
+        for n, _ in st.groups:
+            if (k == 1 and n == "normal") or (k == 2 and n == "opacity"):
+                continue
+            gv = st.grad_view(n)
+            gv.copy_(torch.from_numpy(rng.normal(size=tuple(gv.shape)).astype(np.float32) * 1e-2).to(dev))
+        st.step(adam_fn=adam_fn, absent=("normal",) if k == 1 else ())
+        snaps.append({n: st.view(n).cpu().numpy().copy() for n in ("normal", "opacity", "xyz")})
+        snaps[-1]["m_normal"] = st._view(st.exp_avg, "normal").cpu().numpy().copy()
+    return snaps
+
+
+def _check_absent(snaps, st):
+    # step 1 skipped "normal": param and exp_avg unchanged across it
+    np.testing.assert_array_equal(snaps[1]["normal"], snaps[0]["normal"])
+    np.testing.assert_array_equal(snaps[1]["m_normal"], snaps[0]["m_normal"])
+    assert st.group_steps[[n for n, _ in st.groups].index("normal")] == 2
+    assert st.group_steps[[n for n, _ in st.groups].index("xyz")] == 3
+
+
+def test_step_absent_and_unwritten_groups_cpu(gold):
+    """the gradient buffer is cleared after every step by default (an unwritten group
+    steps with a zero gradient, never the previous one), and `absent` groups are skipped as
+    torch.optim.Adam skips a None grad (per-group step counts)."""
+    import torch
+
+    from relightable3dgaussian_amd import trainer
+
+    st = trainer.GaussianTrainState.from_tensors(_tensors(gold))
+    st.training_setup(_opt_args(), spatial_lr_scale=2.5)
+    snaps = _absent_sequence(st, _cpu_adam_groups, torch.device("cpu"))
+    _check_absent(snaps, st)
+    assert float(st.grad.abs().sum()) == 0.0
+
+
+@pytest.mark.gpu
+def test_gpu_step_absent_matches_oracle(gold, hip_ext):
+    """The HIP Adam (`adam_step_groups`) replays the same absent / unwritten sequence as the oracle."""
+    import torch
+
+    from relightable3dgaussian_amd import trainer
+
+    dev = torch.device("cuda", 0)
+    ref = trainer.GaussianTrainState.from_tensors(_tensors(gold))
+    ref.training_setup(_opt_args(), spatial_lr_scale=2.5)
+    want = _absent_sequence(ref, _cpu_adam_groups, torch.device("cpu"))
+    st = trainer.GaussianTrainState.from_tensors({n: x.to(dev) for n, x in _tensors(gold).items()})
+    st.training_setup(_opt_args(), spatial_lr_scale=2.5)
+    got = _absent_sequence(st, None, dev)
+    _check_absent(got, st)
+    for k in range(3):
+        for n in want[k]:
+            _close(got[k][n].reshape(st.P, -1), want[k][n].reshape(st.P, -1), f"step {k} {n}")
