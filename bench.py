@@ -14,8 +14,8 @@ renders its own camera of the same scene (weak scaling).
 
 Rank 0 prints one JSON line. `roofline` prices renderCUDA fwd + bwd -- render_fwd_glds_kernel,
 render_bwd_glds_kernel and row_sum_kernel (the backward's per-instance reduction) -- with SURVEY.md
-§8d's algorithmic bytes (272*L + 156*H*W + 16*tiles at S=11, + 12*L for the depth sort fused into the
-forward) over their device time, from HIP
+§8d's algorithmic bytes exactly (272*L + 156*H*W + 16*tiles at S=11; the 12*L the forward also moves
+for its fused per-tile depth sort is reported apart, as `extra_bytes`) over their device time, from HIP
 events recorded inside each launch's dispatch on the launch stream during K further steps (the
 timed K steps run without events);
 `traffic` is the HBM bytes of the same kernels from rocprofv3 PMC counters (profiles/, FETCH_SIZE
@@ -43,12 +43,17 @@ P_M1, W_M1, H_M1, S_M1 = 1_000_000, 1920, 1080, 11
 
 
 def algorithmic_bytes(L: int, npix: int, tiles: int, S: int) -> tuple[int, int]:
-    """SURVEY.md §8d per-unit figures: fwd L*(56+4S) + Npix*(40+4S) + 8T, bwd L*(84+8S) + Npix*(28+4S) + 8T;
-    plus 12 L for the forward, which also sorts its tiles (the binning's (depth, id) pairs read, the
-    sorted point_list written: render_fwd.hip fused depth sort)."""
-    fwd = L * (56 + 4 * S + 12) + npix * (40 + 4 * S) + 8 * tiles
+    """SURVEY.md §8d per-unit figures, nothing added: fwd L*(56+4S) + Npix*(40+4S) + 8T,
+    bwd L*(84+8S) + Npix*(28+4S) + 8T."""
+    fwd = L * (56 + 4 * S) + npix * (40 + 4 * S) + 8 * tiles
     bwd = L * (84 + 8 * S) + npix * (28 + 4 * S) + 8 * tiles
     return fwd, bwd
+
+
+def fused_sort_bytes(L: int) -> int:
+    """Bytes the forward blend moves beyond §8d: it also sorts its tiles (the binning's (depth, id)
+    pairs read, 8 B, the sorted point_list written, 4 B per instance; render_fwd.hip)."""
+    return 12 * L
 
 
 def load_traffic() -> dict | None:
@@ -234,6 +239,47 @@ def bvh_visibility(means3D, scales, rots, dev) -> dict:
     return res
 
 
+def comm_probe(P: int, dev, world: int, backend: str, iters: int = 5) -> dict:
+    """The exchange's two collectives alone, at this run's size, outside the timed loop (DESIGN.md
+    §6 cost model): the all-reduce of the 22 dense gradient floats per Gaussian (means3D 3, opacity
+    1, scales 3, rotations 4, features 11) and the all-gather of every view's 3-float SH colour
+    gradient. Mean over `iters` after one warmup, barrier-bracketed, max over ranks. Bus bandwidth
+    as nccl-tests defines it: all-reduce 2(N-1)/N * bytes / t, all-gather (N-1)/N * N * bytes / t."""
+    import torch
+    import torch.distributed as dist
+
+    dense = torch.ones(P * 22, device=dev)
+    col = torch.ones(P, 3, device=dev)
+    buf = torch.empty(world, P, 3, device=dev)
+
+    def gather():
+        if backend == "nccl":
+            dist.all_gather_into_tensor(buf, col)
+        else:
+            dist.all_gather(list(buf.unbind(0)), col)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    t_ar = timed(lambda: dist.all_reduce(dense))
+    t_ag = timed(gather)
+    ar_bytes, ag_bytes = dense.numel() * 4, col.numel() * 4
+    return {"backend": backend, "gaussians": P,
+            "all_reduce_dense22": {"bytes": ar_bytes, "ms": round(t_ar * 1e3, 4),
+                                   "bus_GBps": round(2 * (world - 1) / world * ar_bytes / t_ar / 1e9, 2)},
+            "all_gather_color3": {"bytes_per_rank": ag_bytes, "ms": round(t_ag * 1e3, 4),
+                                  "bus_GBps": round((world - 1) * ag_bytes / t_ag / 1e9, 2)}}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -281,12 +327,12 @@ def main() -> None:
     g_depth = t(rng.normal(size=(H, W)) * 1e-3)
     g_feat = t(rng.normal(size=(S_M1, H, W)) * 1e-3)
 
-    def step():
+    def step(exchange=True):
         out = _C.rasterize_gaussians(bg, 0.0, 0.0, means3D, feats, empty, opac, scales, rots, 1.0, empty, view,
                                      view_inv, proj, proj_inv, cam.tanfovx, cam.tanfovy, cam.cx, cam.cy, H, W, sh, 3,
                                      campos, False, True, None, None, None, None, False)
         L, radii, geom, binning, img = out[0], out[10], out[11], out[12], out[13]
-        if world > 1:
+        if world > 1 and exchange:
             # per-Gaussian gradients all-reduced chunk by chunk, overlapped with the gather phase
             view_parallel.backward_all_reduce(
                 _C, (bg, means3D, feats, radii, empty, scales, rots, 1.0, empty, view, proj, cam.tanfovx,
@@ -298,19 +344,31 @@ def main() -> None:
                                             sh, 3, campos, geom, L, binning, img, True, False)
         return L
 
+    def run(fn, k):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            out = fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0, out
+
     for _ in range(args.warmup):
         L = step()
-    torch.cuda.synchronize()
+    elapsed, L = run(step, args.steps)
+    exchange = None
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        L = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+        # outside the timed region: the same steps without the gradient exchange (each rank's
+        # compute alone, max over ranks) and the two collectives alone at this size
+        t_comp, _ = run(lambda: step(exchange=False), args.steps)
+        tc = torch.tensor([t_comp], dtype=torch.float64, device=dev)
+        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        t_comp = float(tc.item())
+        exchange = comm_probe(args.P, dev, world, backend)
     # per-kernel device times: K more steps with HIP events inside the profiled launches (kept out
     # of the timed region above)
     _C.profile_enable(args.steps + 1)
@@ -338,7 +396,7 @@ def main() -> None:
     launch = {k: (v[1] / v[0] if v[0] else float("nan")) for k, v in prof.items()}
     # renderCUDA fwd + bwd: the backward blend AND its per-instance reduction (row_sum_kernel sums
     # the partial rows the reference accumulates with atomics, backward.cu:552-611)
-    t_kern = (launch["render_fwd"] + launch["render_bwd"] + launch["row_sum"]) / 1e3
+    t_kern = (launch["render_fwd"] + launch["render_bwd"] + launch.get("row_sum", 0.0)) / 1e3
     achieved = (bf + bb) / t_kern / 1e9
     traffic = None
     tr = load_traffic()
@@ -365,12 +423,22 @@ def main() -> None:
                                   f"all-gather of the 3-float SH colour gradient, SH sum rebuilt per rank; "
                                   f"{args.chunks} chunks overlapped with the gather phase)"},
         "views_per_s": round(world * args.steps / elapsed, 3),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        # the blend kernels are bound by neither HBM (frac ~0.14) nor VALU issue (valu.frac ~0.4):
+        # by dependent LDS / exp latency and the batch barrier (DESIGN.md §4 "Can 0.40 be reached")
+        "roofline": {"bound": "latency", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "renderCUDA fwd + bwd: render_fwd_glds_kernel + render_bwd_glds_kernel + row_sum_kernel",
-                     "algorithmic_bytes": bf + bb, "kernel_ms": round(t_kern * 1e3, 4), "valu": valu},
+                     "algorithmic_bytes": bf + bb, "extra_bytes": fused_sort_bytes(L),
+                     "extra_bytes_note": "fused per-tile depth sort in the forward (12 B per instance), not in frac",
+                     "kernel_ms": round(t_kern * 1e3, 4), "valu": valu},
         "kernel_ms": {k: round(v, 4) for k, v in avg.items() if prof[k][0]},
     }
+    if exchange is not None:
+        ms_comp = t_comp / args.steps * 1e3
+        exchange["compute_only_ms_per_step"] = round(ms_comp, 4)
+        exchange["exposed_exchange_ms_per_step"] = round(ms_step - ms_comp, 4)
+        exchange["exposed_frac_of_view"] = round((ms_step - ms_comp) / ms_comp, 4)
+        res["exchange"] = exchange
     if world == 1:
         res["bvh_visibility"] = bvh_visibility(means3D, scales, rots, dev)
     if not args.no_cpu_baseline and world == 1:

@@ -343,6 +343,29 @@ def expf(x):
     return np.array([f(float(v)) for v in x], np.float32)
 
 
+def expf_wide(x):
+    """r3dg_expf_wide, the render equation's exp (render_equation.cu:151 / :351), elementwise."""
+    x = np.ascontiguousarray(x, np.float32).reshape(-1)
+    f = lib().r3dg_expf_wide
+    f.restype = ctypes.c_float
+    f.argtypes = [ctypes.c_float]
+    return np.array([f(float(v)) for v in x], np.float32)
+
+
+def sincosf(x):
+    """r3dg_sincosf, the Fibonacci angle's sin / cos (render_equation.cu:93-94): (sin, cos)."""
+    x = np.ascontiguousarray(x, np.float32).reshape(-1)
+    f = lib().r3dg_sincosf
+    f.restype = None
+    f.argtypes = [ctypes.c_float, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    s, c = ctypes.c_float(), ctypes.c_float()
+    out = np.empty((2, x.size), np.float32)
+    for i, v in enumerate(x):
+        f(float(v), ctypes.byref(s), ctypes.byref(c))
+        out[0, i], out[1, i] = s.value, c.value
+    return out[0], out[1]
+
+
 class blend_exp_libm:
     """Context manager: the oracle's blend uses glibc expf instead of r3dg_expf (measures the exp
     choice; the HIP kernels always use r3dg_expf)."""

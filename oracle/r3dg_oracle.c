@@ -101,6 +101,51 @@ float r3dg_expf(float x)
     return u2f(f2u(p) + (f2u(kf) << 23));
 }
 
+/* render_equation.cu:151 / :351 expf(sharp * (h_d_n - 1)): r3dg_expf's operations over [-87, 88]
+ * (p * 2^k a normal float there), 0 below -87. Identical operation sequence to r3dg_common.h
+ * r3dg_expf_wide. */
+float r3dg_expf_wide(float x)
+{
+    if (x < -87.0f) return 0.0f;
+    x = fminf(x, 88.0f);
+    const float kf = fmaf(x, 0x1.715476p+0f, 0x1.8p+23f);
+    const float k = kf - 0x1.8p+23f;
+    float r = fmaf(k, -0x1.62e400p-1f, x);
+    r = fmaf(k, -0x1.7f7d1cp-20f, r);
+    float p = 0x1.6a959cp-10f;
+    p = fmaf(p, r, 0x1.123a0ap-7f);
+    p = fmaf(p, r, 0x1.555850p-5f);
+    p = fmaf(p, r, 0x1.555492p-3f);
+    p = fmaf(p, r, 0x1.fffffcp-2f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    return u2f(f2u(p) + (f2u(kf) << 23));
+}
+
+/* render_equation.cu:93-94 cosf(theta) / sinf(theta) (CUDA: implementation-defined to 2 ulp):
+ * k = rint(x 2/pi) by the 1.5 * 2^23 shift, r = x - k pi/2 with pi/2 split in three floats (C1 =
+ * 0x1.921fb6p+0, C2 = -0x1.777a5cp-25, C3 = -0x1.ee59dap-50), Cephes minimax sin / cos on
+ * [-pi/4, pi/4], quadrant k mod 4. Identical operation sequence to r3dg_common.h r3dg_sincosf. */
+void r3dg_sincosf(float x, float* s_out, float* c_out)
+{
+    const float kf = fmaf(x, 0x1.45f306p-1f, 0x1.8p+23f);
+    const float k = kf - 0x1.8p+23f;
+    float r = fmaf(k, -0x1.921fb6p+0f, x);
+    r = fmaf(k, 0x1.777a5cp-25f, r);
+    r = fmaf(k, 0x1.ee59dap-50f, r);
+    const float r2 = r * r;
+    float ps = fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f);
+    ps = fmaf(ps, r2, -1.6666654611e-1f);
+    const float sn = fmaf(ps * r2, r, r);
+    float pc = fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f);
+    pc = fmaf(pc, r2, 4.166664568298827e-2f);
+    const float cs = fmaf(pc * r2, r2, fmaf(-0.5f, r2, 1.0f));
+    const uint32_t q = f2u(kf) & 3u;
+    const float a = (q & 1u) ? cs : sn, b = (q & 1u) ? sn : cs;
+    *s_out = (q & 2u) ? -a : a;
+    *c_out = ((q + 1u) & 2u) ? -b : b;
+}
+
 /* The blend's exp: r3dg_expf (mode 0, what the HIP kernels evaluate) or glibc's expf (mode 1, a
  * stand-in for a vendor libm exp such as the reference's CUDA expf, forward.cu:477 / backward.cu:527).
  * Mode 1 exists only to measure how far n_contrib / final_T / the images move when the exp is not
@@ -900,7 +945,9 @@ static void fib_dir(const float* n, int ray, int Ns, float rand01, int use_rand,
     const float rad = sqrtf(1 - z * z);
     float theta = delta * ray;
     if (use_rand) theta = rand01 * 2 * PI_F + theta;
-    const float y = cosf(theta) * rad, x = sinf(theta) * rad;
+    float sn, cs;
+    r3dg_sincosf(theta, &sn, &cs);
+    const float y = cs * rad, x = sn * rad;
     float zs[3] = {x, y, z};
     const float v1 = -n[1], v2 = n[0], v3 = 0.f;
     const float v11 = v1 * v1, v22 = v2 * v2, v33 = v3 * v3, v12 = v1 * v2, v13 = v1 * v3, v23 = v2 * v3;
@@ -945,13 +992,16 @@ static void brdf_eval(int idx, int S_inc, int S_dir, int S_vis, const float* bas
     for (int c = 0; c < 3; ++c) s->fd[c] = (1 - metal) * base[c] / PI_F;
     float r2 = fmaxf(rough * rough, 0.0000001f);
     float amp = 1.0f / (r2 * PI_F), sharp = 2.0f / r2;
-    s->D = amp * expf(sharp * (s->hdn - 1.0f));
-    float p5 = powf(1.0f - s->hdo, 5.0f);
+    s->D = amp * r3dg_expf_wide(sharp * (s->hdn - 1.0f));
+    /* powf(1 - h_d_o, 5) (render_equation.cu:155): CUDA powf's bits are implementation-defined;
+     * stated as products (t^2)^2 t, as brdf.hip */
+    const float t1 = 1.0f - s->hdo, t2 = t1 * t1;
+    float p5 = t2 * t2 * t1;
     for (int c = 0; c < 3; ++c) {
         float F0 = 0.04f * (1.0f - metal) + base[c] * metal;
         s->F[c] = F0 + (1.0f - F0) * p5;
     }
-    float r2v = powf(1.0f + rough, 2.0f) / 8.0f;
+    float r2v = (1.0f + rough) * (1.0f + rough) / 8.0f; /* __powf(1 + rough, 2) / 8 (:158) */
     s->V = (0.5f / fmaxf(s->ndi * (1 - r2v) + r2v, 0.0000001f)) * (0.5f / fmaxf(s->ndo * (1 - r2v) + r2v, 0.0000001f));
     for (int c = 0; c < 3; ++c) s->fs[c] = s->D * s->F[c] * s->V;
 }
@@ -1040,6 +1090,10 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
                                      float* d_inc, float* d_dir, float* d_vis)
 {
     const float K = 2.0f * PI_F / (float)Ns;
+    /* dL_ddirect_shs: the reference's racy float += over every (Gaussian, sample) (:443-445) has
+     * no defined value; here it is the exact sum (double accumulation, rounded once), which any
+     * fixed-order float reduction approaches to its own rounding */
+    double ddir_acc[16 * 3] = {0};
     for (int idx = 0; idx < P; ++idx) {
         const float* n = normals + 3 * idx;
         const float* v = viewdirs + 3 * idx;
@@ -1055,8 +1109,8 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             brdf_eval(idx, S_inc, S_dir, S_vis, b, rough_i, metal_i, n, v, inc, dir_shs, vis_shs, d, coef, &s);
             float r2 = fmaxf(rough_i * rough_i, 0.0000001f);
             float amp = 1.0f / (r2 * PI_F), sharp = 2.0f / r2;
-            float e_amp = expf(sharp * (s.hdn - 1.0f));
-            float r2v = powf(1.0f + rough_i, 2.0f) / 8.0f;
+            float e_amp = r3dg_expf_wide(sharp * (s.hdn - 1.0f));
+            float r2v = (1.0f + rough_i) * (1.0f + rough_i) / 8.0f; /* powf(1 + rough, 2) / 8 (:359) */
             float den1 = fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f);
             float den2 = fmaxf(s.ndo * (1 - r2v) + r2v, 0.0000001f);
             float g1 = 0.5f / den1, g2 = 0.5f / den2;
@@ -1083,7 +1137,9 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             float dhdn = sharp * e_amp * de;
             float dr2 = -2.0f / (r2 * r2) * dsharp - 1.0f / (r2 * r2 * PI_F) * damp;
             float drough = dr2 * 2.0f * rough_i;
-            float p5 = powf(1.0f - s.hdo, 5.0f), p4 = powf(1.0f - s.hdo, 4.0f);
+            /* powf(1 - h_d_o, 5 / 4) (:394-395) as products, as brdf_eval */
+            const float t1 = 1.0f - s.hdo, t2 = t1 * t1;
+            float p4 = t2 * t2, p5 = p4 * t1;
             float dF0[3], dhdo = 0;
             for (int c = 0; c < 3; ++c) {
                 float F0 = 0.04f * (1.0f - metal_i) + b[c] * metal_i;
@@ -1110,8 +1166,8 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             for (int c = 0; c < 3; ++c) dvis_s += dli[c] * s.global[c];
             for (int i = 0; i < S_vis; ++i) d_vis[(size_t)idx * S_vis + i] += dvis_s * coef[i];
             /* clamp checks after fmaxf never fire (render_equation.cu:440-449, bug-compatible) */
-            for (int i = 0; i < S_dir; ++i)
-                for (int c = 0; c < 3; ++c) d_dir[i * 3 + c] += dglob[c] * coef[i];
+            for (int i = 0; i < S_dir && i < 16; ++i)
+                for (int c = 0; c < 3; ++c) ddir_acc[i * 3 + c] += (double)(dglob[c] * coef[i]);
             for (int i = 0; i < S_dir; ++i) /* loop bound S_direct, render_equation.cu:450 */
                 for (int c = 0; c < 3; ++c) d_inc[((size_t)idx * S_inc + i) * 3 + c] += dli[c] * coef[i];
             for (int c = 0; c < 3; ++c) {
@@ -1123,6 +1179,8 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             d_rough[idx] += drough;
         }
     }
+    for (int i = 0; i < S_dir && i < 16; ++i)
+        for (int c = 0; c < 3; ++c) d_dir[i * 3 + c] += (float)ddir_acc[i * 3 + c];
 }
 
 /* batch entry points for the golden-vector tests of the per-Gaussian sub-steps */

@@ -32,7 +32,10 @@ HIP_FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall", "-W
 # the key path (projection, radius, rect) must not contract a*b+c into fma: see preprocess.hip
 # render_bwd: the SLP vectorizer pairs the two unrolled blend steps into packed f32 ops plus
 # register shuffles (more instructions, 30 more VGPRs); plain scalar code measures faster
-PER_FILE_FLAGS = {"preprocess.hip": ["-ffp-contract=off"], "bvh.hip": ["-ffp-contract=off"], "render_bwd.hip": ["-fno-slp-vectorize"]}
+# brdf.hip: the render equation restates the oracle's operation sequence (no a*b+c contraction), so
+# the BRDF outputs are bit-identical to it
+PER_FILE_FLAGS = {"preprocess.hip": ["-ffp-contract=off"], "bvh.hip": ["-ffp-contract=off"],
+                  "brdf.hip": ["-ffp-contract=off"], "render_bwd.hip": ["-fno-slp-vectorize"]}
 
 
 def _newer(target: str, deps: list[str]) -> bool:

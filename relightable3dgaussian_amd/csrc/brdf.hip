@@ -36,7 +36,9 @@ __device__ __forceinline__ float3 fib_dir(float3 n, int ray, int Ns, float rot) 
     const float z = 1 - 2 * (float)ray / (2 * (float)Ns - 1);
     const float rad = sqrtf(1 - z * z);
     const float theta = rot + delta * ray;
-    const float y = cosf(theta) * rad, x = sinf(theta) * rad;
+    float sn, cs;
+    r3dg_sincosf(theta, &sn, &cs);  // bit-identical to the oracle's (r3dg_common.h)
+    const float y = cs * rad, x = sn * rad;
     const float v1 = -n.y, v2 = n.x, v3 = 0.f;
     const float v11 = v1 * v1, v22 = v2 * v2, v33 = v3 * v3, v12 = v1 * v2, v13 = v1 * v3, v23 = v2 * v3;
     const float cp1 = fmaxf(n.z + 1, 0.0000001f);
@@ -51,7 +53,7 @@ struct Sample {
     float local[3], global[3], vis, light[3];
     float hdn, hdo, ndi, ndo, half_norm, half[3];
     float fd[3], fs[3], D, F[3], V;
-    float e_amp, inv_half_norm;  // eval_brdf_fast only
+    float e_amp;
 };
 
 struct GaussBRDF {
@@ -100,7 +102,14 @@ __device__ __forceinline__ void eval_lights(const float* coef, const float* inc,
     for (int c = 0; c < 3; ++c) s.light[c] = s.vis * s.global[c] + s.local[c];
 }
 
-__device__ __forceinline__ void eval_brdf(const GaussBRDF& G, float3 d, Sample& s) {
+// render_equation.cu:138-161 for one sample, with the per-Gaussian terms (amp, sharp, r2v, the
+// view-side GGX factor g2 = 0.5 / denom2) hoisted by the caller -- the same IEEE operations in the
+// same order as the oracle's brdf_eval (true divisions, FP contraction off for this file), so D,
+// F, V and f_d / f_s are bit-identical to it. The reference's transcendentals (expf, powf; their
+// bits are CUDA-implementation-defined) are stated once for both: r3dg_expf_wide, and powf(t, 5)
+// as the products (t^2)^2 t.
+__device__ __forceinline__ void eval_brdf(const GaussBRDF& G, float3 d, float amp, float sharp, float r2v, float g2,
+                                          Sample& s) {
     const float hx = d.x + G.v.x, hy = d.y + G.v.y, hz = d.z + G.v.z;
     s.half_norm = fmaxf(sqrtf(hx * hx + hy * hy + hz * hz), 0.0000001f);
     s.half[0] = hx / s.half_norm; s.half[1] = hy / s.half_norm; s.half[2] = hz / s.half_norm;
@@ -109,44 +118,13 @@ __device__ __forceinline__ void eval_brdf(const GaussBRDF& G, float3 d, Sample& 
     s.ndi = fmaxf(G.n.x * d.x + G.n.y * d.y + G.n.z * d.z, 0.0f);
     s.ndo = fmaxf(G.n.x * G.v.x + G.n.y * G.v.y + G.n.z * G.v.z, 0.0f);
     const float base[3] = {G.base.x, G.base.y, G.base.z};
-    const float r2 = fmaxf(G.rough * G.rough, 0.0000001f);
-    const float amp = 1.0f / (r2 * kPi), sharp = 2.0f / r2;
-    s.D = amp * expf(sharp * (s.hdn - 1.0f));
-    const float p5 = powf(1.0f - s.hdo, 5.0f);
-    const float r2v = powf(1.0f + G.rough, 2.0f) / 8.0f;
-    s.V = (0.5f / fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f)) * (0.5f / fmaxf(s.ndo * (1 - r2v) + r2v, 0.0000001f));
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        s.fd[c] = (1 - G.metal) * base[c] * (1.0f / kPi);
-        const float F0 = 0.04f * (1.0f - G.metal) + base[c] * G.metal;
-        s.F[c] = F0 + (1.0f - F0) * p5;
-        s.fs[c] = s.D * s.F[c] * s.V;
-    }
-}
-
-// eval_brdf for the backward: the per-Gaussian terms (amp, sharp, r2v, the view-side GGX factor
-// g2) hoisted by the caller, reciprocal multiplications for the sample's divisions and products
-// for powf(x, 5) (agrees with eval_brdf to ~1e-6 relative).
-__device__ __forceinline__ void eval_brdf_fast(const GaussBRDF& G, float3 d, float amp, float sharp, float r2v,
-                                               float g2, Sample& s) {
-    const float hx = d.x + G.v.x, hy = d.y + G.v.y, hz = d.z + G.v.z;
-    s.half_norm = fmaxf(sqrtf(hx * hx + hy * hy + hz * hz), 0.0000001f);
-    // the half vector by true divisions, as eval_brdf: the sharp specular lobe (sharp = 2 / r^2,
-    // 800 at roughness 0.05) amplifies an ulp of h.n into 1e-4 of the roughness gradient
-    s.inv_half_norm = __builtin_amdgcn_rcpf(s.half_norm);
-    s.half[0] = hx / s.half_norm; s.half[1] = hy / s.half_norm; s.half[2] = hz / s.half_norm;
-    s.hdn = fmaxf(s.half[0] * G.n.x + s.half[1] * G.n.y + s.half[2] * G.n.z, 0.0f);
-    s.hdo = fmaxf(s.half[0] * G.v.x + s.half[1] * G.v.y + s.half[2] * G.v.z, 0.0f);
-    s.ndi = fmaxf(G.n.x * d.x + G.n.y * d.y + G.n.z * d.z, 0.0f);
-    s.ndo = fmaxf(G.n.x * G.v.x + G.n.y * G.v.y + G.n.z * G.v.z, 0.0f);
-    const float base[3] = {G.base.x, G.base.y, G.base.z};
-    s.e_amp = __expf(sharp * (s.hdn - 1.0f));
+    s.e_amp = r3dg_expf_wide(sharp * (s.hdn - 1.0f));
     s.D = amp * s.e_amp;
     const float t1 = 1.0f - s.hdo, t2 = t1 * t1, p5 = t2 * t2 * t1;
-    s.V = (0.5f * __builtin_amdgcn_rcpf(fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f))) * g2;
+    s.V = (0.5f / fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f)) * g2;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        s.fd[c] = (1 - G.metal) * base[c] * (1.0f / kPi);
+        s.fd[c] = (1 - G.metal) * base[c] / kPi;
         const float F0 = 0.04f * (1.0f - G.metal) + base[c] * G.metal;
         s.F[c] = F0 + (1.0f - F0) * p5;
         s.fs[c] = s.D * s.F[c] * s.V;
@@ -225,7 +203,7 @@ __global__ void __launch_bounds__(256) brdf_fwd_kernel(BrdfKArgs a) {
             eval_lights<NI, ND, NV>(coef, inc_r, NI, in.direct_shs, ND, vis_r, NV, s);
         else
             eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, in.direct_shs, in.S_direct, vis_g, in.S_visibility, s);
-        eval_brdf_fast(G, d, amp, sharp, r2v, g2, s);
+        eval_brdf(G, d, amp, sharp, r2v, g2, s);
         const float tmp = 2.0f * kPi * s.ndi / (float)Ns;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -309,7 +287,6 @@ brdf_bwd_kernel(BrdfKArgs a) {
         const float* inc_g = in.incidents_shs + (size_t)idx * 3 * in.S_incident;
         const float* vis_g = in.visibility_shs + (size_t)idx * in.S_visibility;
         const int Ns = in.sample_num;
-        const float K = 2.0f * kPi / (float)Ns;
         const float gp[3] = {a.dL_dpbr[3 * idx], a.dL_dpbr[3 * idx + 1], a.dL_dpbr[3 * idx + 2]};
         const float gdl[3] = {a.dL_ddiff[3 * idx], a.dL_ddiff[3 * idx + 1], a.dL_ddiff[3 * idx + 2]};
         const float n[3] = {G.n.x, G.n.y, G.n.z}, v[3] = {G.v.x, G.v.y, G.v.z};
@@ -358,11 +335,11 @@ brdf_bwd_kernel(BrdfKArgs a) {
                 eval_lights<NI, ND, NV>(coef, inc_r, NI, env, ND, vis_r, NV, s);
             else
                 eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, env, S_dir, vis_g, in.S_visibility, s);
-            eval_brdf_fast(G, d, amp, sharp, r2v, g2, s);
+            eval_brdf(G, d, amp, sharp, r2v, g2, s);
             const float e_amp = s.e_amp;
             const float den1 = fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f);
-            const float g1 = 0.5f * __builtin_amdgcn_rcpf(den1);
-            const float Tn = s.ndi * K;
+            const float g1 = 0.5f / den1;
+            const float Tn = 2.0f * kPi * s.ndi / (float)Ns;
             float dfd[3], dfs[3], dli[3], fsum[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -371,16 +348,13 @@ brdf_bwd_kernel(BrdfKArgs a) {
                 dfs[c] = gp[c] * s.light[c] * Tn;
                 dli[c] = gp[c] * fsum[c] * Tn;
             }
-            float dndi = (gp[0] * (fsum[0] * s.light[0]) + gp[1] * (fsum[1] * s.light[1]) +
-                          gp[2] * (fsum[2] * s.light[2])) * K;
 #pragma unroll
             for (int c = 0; c < 3; ++c) dli[c] += gdl[c] * Tn;
-            dndi += gdl[0] * (s.light[0] * K) + gdl[1] * (s.light[1] * K) + gdl[2] * (s.light[2] * K);
-            (void)dndi;  // overwritten below, as in the reference (:403)
+            // dL_dn_d_i of :372 / :376 is overwritten at :403 before any use (bug-compatible): not formed
             float dbase[3];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) dbase[c] = dfd[c] * ((1 - metal) * (1.0f / kPi));
-            float dmetal = -(dfd[0] * b[0] + dfd[1] * b[1] + dfd[2] * b[2]) * (1.0f / kPi);
+            for (int c = 0; c < 3; ++c) dbase[c] = dfd[c] * (1 - metal) / kPi;
+            float dmetal = -(dfd[0] * b[0] + dfd[1] * b[1] + dfd[2] * b[2]) / kPi;
             const float dD = dfs[0] * s.V * s.F[0] + dfs[1] * s.V * s.F[1] + dfs[2] * s.V * s.F[2];
             float dF[3];
 #pragma unroll
@@ -404,7 +378,7 @@ brdf_bwd_kernel(BrdfKArgs a) {
             for (int c = 0; c < 3; ++c) dbase[c] += metal * dF0[c];
             dmetal += (b[0] - 0.04f) * dF0[0] + (b[1] - 0.04f) * dF0[1] + (b[2] - 0.04f) * dF0[2];
             const float dg1 = dV * g2, dg2 = dV * g1;
-            const float dden1 = -2.0f * (g1 * g1) * dg1, dden2 = -2.0f * (g2 * g2) * dg2;
+            const float dden1 = -0.5f / (den1 * den1) * dg1, dden2 = -0.5f / (den2 * den2) * dg2;
             const float dndi2 = dden1 * (1 - r2v);
             const float dndo = dden2 * (1 - r2v);
             const float dr2v = (1.0f - s.ndi) * dden1 + (1.0f - s.ndo) * dden2;
@@ -427,7 +401,7 @@ brdf_bwd_kernel(BrdfKArgs a) {
                 for (int c = 0; c < 3; ++c) { dn[c] += v[c] * dndo; dv[c] += n[c] * dndo; }
             }
 #pragma unroll
-            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] * s.inv_half_norm;
+            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] / s.half_norm;
             float dglob[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) dglob[c] = dli[c] * s.vis;
@@ -563,7 +537,7 @@ __global__ void __launch_bounds__(256) brdf_fwd_lane_kernel(BrdfKArgs a, int GB)
             eval_lights<NI, ND, NV>(coef, inc_r, NI, in.direct_shs, ND, vis_r, NV, s);
         else
             eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, in.direct_shs, in.S_direct, vis_g, in.S_visibility, s);
-        eval_brdf_fast(G, d, amp, sharp, r2v, g2, s);
+        eval_brdf(G, d, amp, sharp, r2v, g2, s);
         const float tmp = 2.0f * kPi * s.ndi / (float)Ns;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {

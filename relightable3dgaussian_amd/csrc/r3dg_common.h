@@ -244,6 +244,55 @@ __device__ __forceinline__ float r3dg_expf(float x) {
     return __uint_as_float(__float_as_uint(p) + (__float_as_uint(kf) << 23));
 }
 
+// The render equation's exp (render_equation.cu:151 / :351 `expf(sharp * (h_d_n - 1))`: the
+// argument reaches -2e7 at the roughness floor and a few ulp above 0 when |h|·|n| rounds above 1).
+// r3dg_expf's operations over [-87, 88] -- where p·2^k stays a normal float, so the exponent add
+// is exact -- and 0 below -87 (e^-87 = 1.6e-38: the reference's denormal results differ from 0 by
+// less than amp · 2^-126). Restated by oracle/r3dg_oracle.c r3dg_expf_wide.
+__device__ __forceinline__ float r3dg_expf_wide(float x) {
+#pragma clang fp contract(off)
+    if (x < -87.0f) return 0.0f;
+    x = fminf(x, 88.0f);
+    const float kf = __builtin_fmaf(x, 0x1.715476p+0f, 0x1.8p+23f);
+    const float k = kf - 0x1.8p+23f;
+    float r = __builtin_fmaf(k, -0x1.62e400p-1f, x);
+    r = __builtin_fmaf(k, -0x1.7f7d1cp-20f, r);
+    float p = 0x1.6a959cp-10f;
+    p = __builtin_fmaf(p, r, 0x1.123a0ap-7f);
+    p = __builtin_fmaf(p, r, 0x1.555850p-5f);
+    p = __builtin_fmaf(p, r, 0x1.555492p-3f);
+    p = __builtin_fmaf(p, r, 0x1.fffffcp-2f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    return __uint_as_float(__float_as_uint(p) + (__float_as_uint(kf) << 23));
+}
+
+// sin and cos of the Fibonacci sample angle (render_equation.cu:93-94 `cosf(theta)`, `sinf(theta)`;
+// CUDA's are implementation-defined to 2 ulp). One bit-reproducible f32 statement shared with the
+// oracle (oracle/r3dg_oracle.c r3dg_sincosf): k = rint(x · 2/π) by the 1.5 · 2^23 shift,
+// three-term Cody-Waite reduction r = x - k·π/2 (π/2 = C1 + C2 + C3, each product singly rounded
+// by an FMA), the Cephes minimax polynomials for sin / cos on [-π/4, π/4], quadrant k mod 4.
+// |x| < 2^15 (angles reach 2.4 · Ns + 2π).
+__device__ __forceinline__ void r3dg_sincosf(float x, float* s_out, float* c_out) {
+#pragma clang fp contract(off)
+    const float kf = __builtin_fmaf(x, 0x1.45f306p-1f, 0x1.8p+23f);
+    const float k = kf - 0x1.8p+23f;
+    float r = __builtin_fmaf(k, -0x1.921fb6p+0f, x);
+    r = __builtin_fmaf(k, 0x1.777a5cp-25f, r);
+    r = __builtin_fmaf(k, 0x1.ee59dap-50f, r);
+    const float r2 = r * r;
+    float ps = __builtin_fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f);
+    ps = __builtin_fmaf(ps, r2, -1.6666654611e-1f);
+    const float sn = __builtin_fmaf(ps * r2, r, r);
+    float pc = __builtin_fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f);
+    pc = __builtin_fmaf(pc, r2, 4.166664568298827e-2f);
+    const float cs = __builtin_fmaf(pc * r2, r2, __builtin_fmaf(-0.5f, r2, 1.0f));
+    const unsigned q = __float_as_uint(kf) & 3u;
+    const float a = (q & 1u) ? cs : sn, b = (q & 1u) ? sn : cs;
+    *s_out = (q & 2u) ? -a : a;
+    *c_out = ((q + 1u) & 2u) ? -b : b;
+}
+
 // r3dg_expf on two values with packed f32 ops (v_pk_fma_f32 / v_pk_add_f32): per component the
 // same IEEE operations in the same order, so each result is bit-identical to r3dg_expf.
 __device__ __forceinline__ f32x2 r3dg_expf2(float x0, float x1) {

@@ -84,3 +84,20 @@ def assert_close(name, a, b, atol, rtol=0.0):
     bad = d > (atol + rtol * np.abs(b.astype(np.float64)))
     assert not bad.any(), (f"{name}: {int(bad.sum())}/{bad.size} elements off, max abs diff {d.max():.3e} "
                            f"(atol {atol}, rtol {rtol}) at {np.unravel_index(np.argmax(d), d.shape)}")
+
+
+def assert_brdf(name, got, ref, summed=False):
+    """The render equation's outputs against the oracle at north_star's bar: 1e-4 abs, no relative
+    slack. brdf.hip and the oracle evaluate the same IEEE operation sequence (shared sin / cos /
+    exp statements, contraction off), so every per-Gaussian output is expected bit-identical; the
+    count of differing elements is printed. `summed`: dL_ddirect_shs, a sum over every (Gaussian,
+    sample) whose order differs (block tree vs the oracle's exact sum): 1e-4 relative to its scale
+    (max |ref|)."""
+    got = np.asarray(got)
+    ref = np.asarray(ref)
+    d = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+    print(f"brdf {name}: {int((got != ref).sum())}/{got.size} differ, max abs diff {d.max() if d.size else 0:.3e}")
+    if summed:
+        assert_close(name, got, ref, 1e-4 * max(float(np.abs(ref).max()), 1e-12), 1e-4)
+    else:
+        assert_close(name, got, ref, 1e-4, 0.0)

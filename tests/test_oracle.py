@@ -344,3 +344,28 @@ def test_brdf_torch_pi5_matches_cuda_path_fixture():
                                             t["incidents"], t["env"], t["visibility"], int(g["sample_num"]),
                                             pi=3.14159)
     _close("pbr", pbr.numpy(), g["pbr"], 2e-5, 1e-4)
+
+
+def test_brdf_transcendentals_are_faithful():
+    """The render equation's sin / cos / exp (r3dg_sincosf, r3dg_expf_wide: one f32 statement shared
+    bit for bit by the oracle and brdf.hip, replacing CUDA sinf / cosf / expf whose bits no file of
+    the reference pins): within 2 ulp-of-1 of double sin / cos over every Fibonacci angle the call
+    sites produce (2.4 r + 2 pi u, Ns <= 256) and known answers; exp within 1 ulp over [-87, 0.01]
+    and 0 below -87."""
+    rng = np.random.default_rng(0)
+    delta = np.float32(np.float32(3.14159) * (np.float32(3.0) - np.sqrt(np.float32(5.0))))
+    r = np.arange(256, dtype=np.float32)
+    x = np.concatenate([delta * r, (delta * r[:24])[None, :] + rng.uniform(0, 2 * 3.14159, (200, 24)).astype(np.float32)
+                        .reshape(200, 24), rng.uniform(-700, 700, 5000)], axis=None).astype(np.float32)
+    x = np.concatenate([x, np.array([0.0, np.pi / 4, np.pi / 2, np.pi, 3 * np.pi / 2, 2 * np.pi, -1.0], np.float32)])
+    s, c = oracle.sincosf(x)
+    xd = x.astype(np.float64)
+    assert np.abs(s - np.sin(xd)).max() <= 2 * 2.0 ** -24, np.abs(s - np.sin(xd)).max()
+    assert np.abs(c - np.cos(xd)).max() <= 2 * 2.0 ** -24, np.abs(c - np.cos(xd)).max()
+    assert oracle.sincosf(np.float32([0.0]))[0][0] == 0.0 and oracle.sincosf(np.float32([0.0]))[1][0] == 1.0
+    e = np.concatenate([np.linspace(-87.0, 0.01, 20001), [-87.5, -800.0, -2e7]]).astype(np.float32)
+    got = oracle.expf_wide(e).astype(np.float64)
+    ref = np.where(e < -87.0, 0.0, np.exp(e.astype(np.float64)))
+    ok = e >= -87.0
+    assert np.all(np.abs(got[ok] - ref[ok]) <= np.spacing(ref[ok].astype(np.float32)))
+    assert np.all(got[~ok] == 0.0)
