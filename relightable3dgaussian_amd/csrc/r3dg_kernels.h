@@ -91,6 +91,9 @@ struct RenderFwdArgs {
     // to point_list_out; null pairs: every tile was sorted by tile_depth_sort_kernel
     const uint2* pairs;
     uint32_t* point_list_out;
+    // non-default splat shaders: per Gaussian float4 [shader r, g, b, 0] (refresh_record_opacity
+    // writes it after the splat shaders), staged as one more record column
+    const float4* shader_rec;
 };
 constexpr int kFusedSortMax = 1024;
 
@@ -135,6 +138,9 @@ struct RenderBwdArgs {
     float* rows;               // [4L, RS] partial rows (part_row_stride)
     uint8_t* flags;            // [4L] 1 where a partial row was written (zeroed by the forward's binning scatter)
     const uint8_t* contrib;    // [L] the forward's contribution bits (RenderFwdArgs::contrib)
+    int sums_atomic;           // 1: flush straight into `sums` with f32 atomics (no rows / flags)
+    float* sums;               // [P, SRS] per-Gaussian sums, zeroed before the launch (sums_atomic)
+    int SRS;
 };
 
 struct GatherBwdArgs {
@@ -142,6 +148,8 @@ struct GatherBwdArgs {
     int g_begin, g_end;       // Gaussian range of this launch (outputs indexed by global id)
     const float* rows;        // partial rows (RenderBwdArgs)
     float* sums;              // [P, RS] per-Gaussian sums (row_sum_kernel -> gather_bwd_kernel)
+    int sums_moments;         // 1: sums hold the raw moments about the mean (atomic flush), stride SRS
+    int SRS;
     const uint32_t* flags;    // one word per slot: byte q set when quadrant q's row exists
     const float2* means2D;
     const float4* conic_opacity;

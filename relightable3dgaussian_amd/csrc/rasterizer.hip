@@ -229,12 +229,17 @@ __global__ void __launch_bounds__(256) init_stencil_kernel(int P, float* stencil
 
 // Splat shaders edit conic_opacity.w after the render records were written: refresh the records'
 // opacity (the backward reads records; the reference's backward reads the edited geometry state).
+// Also packs the splat shaders' colour into one float4 per Gaussian, the shader blend's extra
+// staged record column (render_fwd_glds_kernel<SMAX, true>).
 __global__ void __launch_bounds__(256) refresh_record_opacity_kernel(int P, const int* __restrict__ radii,
                                                                      const float4* __restrict__ conic_opacity,
-                                                                     float4* __restrict__ records, int rec4) {
+                                                                     float4* __restrict__ records, int rec4,
+                                                                     const float* __restrict__ shader_rgb,
+                                                                     float4* __restrict__ shader_rec) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P || radii[i] <= 0) return;
     records[(size_t)i * rec4].w = conic_opacity[i].w;
+    shader_rec[i] = make_float4(shader_rgb[3 * i], shader_rgb[3 * i + 1], shader_rgb[3 * i + 2], 0.f);
 }
 
 // ---- shader registry (ShShader.cu:196-230, splatShader.cu:283-333, postProcessShader.cu:395-436) ----
@@ -476,7 +481,10 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     const size_t M3 = (size_t)3 * (g->sh ? s->M : 0);
     const size_t work_floats = work_copies ? (size_t)P * (3 + 3 + 4 + 1 + M3 + S) : 0;
     const size_t post_floats = post_blur ? (size_t)3 * H * W : 0;  // BlurLighting's incident-light snapshot
-    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * (work_floats + post_floats));
+    // the splat shaders' colour as one float4 per Gaussian (16-B aligned, after the other extras)
+    const size_t shrec_off = (work_floats + post_floats + 3) & ~(size_t)3;
+    const size_t shrec_floats = splat_active ? 4 * (size_t)P : 0;
+    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * (shrec_off + shrec_floats));
     // with a scratch allocator the binning's tile counts are transient (needed only until the
     // scatter), not part of the image state autograd keeps alive until the backward
     const bool hist_scratch = scratch_alloc != nullptr && P > 0;
@@ -487,6 +495,9 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         return R3DG_ERR_ALLOC;
     }
     GeomState geom = geom_state_from(geom_base, (size_t)P, S);
+    float4* shader_rec =
+        splat_active ? reinterpret_cast<float4*>(static_cast<char*>(geom_base) + geom_bytes + sizeof(float) * shrec_off)
+                     : nullptr;
     ImageState img = carve_image((uintptr_t)img_base, H, W, nullptr, !hist_scratch);
     if (hist_scratch) img.bin_hist = hist_base;
     int* radii = out->radii ? out->radii : geom.internal_radii;
@@ -662,7 +673,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
             R3DG_CHECK_LAUNCH(s->debug, st);
         }
         hipLaunchKernelGGL(refresh_record_opacity_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, radii,
-                           geom.conic_opacity, geom.records, record_f4(S));
+                           geom.conic_opacity, geom.records, record_f4(S), geom.shader_rgb, shader_rec);
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
@@ -693,6 +704,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     ra.contrib = bin.contrib;
     ra.pairs = splat_active ? nullptr : bin.pairs;  // fused depth sort (render_fwd_glds_kernel)
     ra.point_list_out = bin.point_list;
+    ra.shader_rec = shader_rec;
     if (const char* e = getenv("R3DG_NO_CULL")) ra.cull = (e[0] == '0');
     {
         ProfScope ps(R3DG_PROF_RENDER_FWD, st);
@@ -774,15 +786,28 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     // forward's duplicate pass (a row's presence depends on the forward state only)
     // the backward blend addresses partial rows with 32-bit offsets in float4 units
     R3DG_REQUIRE((size_t)RS * (size_t)L < (1ull << 32), "rasterize_gaussians_backward: too many tile instances");
-    const size_t row_bytes = sizeof(float) * (size_t)RS * 4 * L;
-    const size_t sum_bytes = sizeof(float) * (size_t)RS * P;
+    // R3DG_BWD_REDUCE=atomic: the backward blend adds its (instance, wave) rows into the per-Gaussian
+    // sums with f32 atomics (no partial rows, flags or row_sum_kernel; order-dependent last bits)
+    const bool atomic_sums = [] {
+        const char* e = getenv("R3DG_BWD_REDUCE");  // read per call: tests switch it at run time
+        return e && e[0] == 'a';
+    }();
+    // atomic sums: [X part | 6 moments | pad] per Gaussian, rows of 32 floats (128 B) so each
+    // 16-float X segment is one aligned 64-B atomic request
+    const int SRS = (RS + 31) & ~31;
+    const size_t row_bytes = atomic_sums ? 0 : sizeof(float) * (size_t)RS * 4 * L;
+    const size_t sum_bytes = sizeof(float) * (size_t)(atomic_sums ? SRS : RS) * P;
     char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + sum_bytes);
     if (!scratch) {
         set_error("rasterize_gaussians_backward: scratch allocation failed");
         return R3DG_ERR_ALLOC;
     }
-    float* rows = L > 0 ? reinterpret_cast<float*>(scratch) : nullptr;
+    float* rows = L > 0 && !atomic_sums ? reinterpret_cast<float*>(scratch) : nullptr;
     float* sums = reinterpret_cast<float*>(scratch + row_bytes);
+    if (atomic_sums) {
+        ProfScope ps(R3DG_PROF_ROW_SUM, st);
+        R3DG_CHECK_HIP(hipMemsetAsync(sums, 0, sum_bytes, st));
+    }
     uint8_t* flags = reinterpret_cast<uint8_t*>(bs.flags);
     if (L > 0) {
         RenderBwdArgs ba{};
@@ -817,6 +842,9 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         ba.rows = rows;
         ba.flags = flags;
         ba.contrib = bs.contrib;
+        ba.sums_atomic = atomic_sums;
+        ba.sums = sums;
+        ba.SRS = SRS;
         {
             ProfScope ps(R3DG_PROF_RENDER_BWD, st);
             R3DG_CHECK_HIP(launch_render_backward(ba, st));
@@ -828,6 +856,8 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     ga.W = W; ga.H = H; ga.grid_x = gx; ga.grid_y = gy;
     ga.rows = rows;
     ga.sums = sums;
+    ga.sums_moments = atomic_sums;
+    ga.SRS = SRS;
     ga.flags = reinterpret_cast<const uint32_t*>(flags);
     ga.means2D = gs.means2D;
     ga.conic_opacity = gs.conic_opacity;
@@ -864,7 +894,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     for (int c = 0, g0 = 0; g0 < P; ++c, g0 += per) {
         ga.g_begin = g0;
         ga.g_end = std::min(P, g0 + per);
-        {
+        if (!atomic_sums) {
             ProfScope ps(R3DG_PROF_ROW_SUM, st);
             R3DG_CHECK_HIP(launch_row_sum(ga, st));
         }

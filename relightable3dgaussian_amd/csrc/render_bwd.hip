@@ -299,7 +299,12 @@ __device__ __forceinline__ void split_bf16x3(const float (&x)[8], bf16x8& h, bf1
 // the lane that loaded its bits (record_slot), so nothing but the records goes through LDS.
 // Staging buffer layout: column q (float4 q of the record) of instance t at [q * NB + t].
 // ---------------------------------------------------------------------------------------------
-template <int SMAX>
+// ATOM: the reduction's second stage in the flush itself -- each (instance, wave) row is expanded
+// about the Gaussian's mean and added with no-return f32 atomics into the per-Gaussian sums
+// [P, SRS] (the reference's own accumulation, backward.cu:552-611, at one atomic per channel per
+// (instance, wave) instead of per pixel): no partial rows, no row flags, no row_sum_kernel; sums
+// depend on the atomics' arrival order. !ATOM: the deterministic partial rows + row_sum_kernel.
+template <int SMAX, bool ATOM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
 render_bwd_glds_kernel(RenderBwdArgs a) {
     constexpr int NB = R3DG_BWDG_NB;              // instances per batch (two batches staged)
@@ -377,7 +382,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     }
     float u = 0.f;
     const float TFB = T_final * bg_dot;
-    int rowj = 0;  // group row r's partial-row index (4 * slot + quadrant) in lane r
+    int rowj = 0;  // group row r's partial-row index (4 * slot + quadrant) in lane r (ATOM: its Gaussian)
+    float d0xr = 0.f, d0yr = 0.f;  // ATOM: group row r's mean - quadrant centre in lane r
     const float qcx = (float)(tx * kTileX + (w & 1) * 8) + 3.5f, qcy = (float)(ty * kTileY + (w >> 1) * 8) + 3.5f;
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
     const int max_last = block_max_last(wmax, s_max_last);
@@ -474,6 +480,34 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, yb[b], accY, 0, 0, 0);
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o, yb[b], accY, 0, 0, 0);
         }
+        if constexpr (ATOM) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = (l >> 4) * 4 + i;
+                const uint32_t gid = (uint32_t)__shfl(rowj, row);
+                const float d0x = __shfl(d0xr, row), d0y = __shfl(d0yr, row);
+                // the row's moments about the quadrant centre, S0 / Sx / Sy from lanes 0..2 of the row
+                const float s0 = __shfl(accY[i], l & 48), s1 = __shfl(accY[i], (l & 48) + 1),
+                            s2 = __shfl(accY[i], (l & 48) + 2);
+                if (row < r) {
+                    float* dst = a.sums + (size_t)gid * a.SRS;
+#pragma unroll
+                    for (int xb = 0; xb < NXB; ++xb)
+                        if (xb * 16 + nch < 4 + S) atomicAdd(dst + xb * 16 + nch, accX[xb][i]);
+                    // expand_moments, one output per lane (the same operations as row_sum_kernel's)
+                    const float sk = accY[i];
+                    float e = s0;
+                    if (nch == 1) e = d0x * s0 - s1;
+                    else if (nch == 2) e = d0y * s0 - s2;
+                    else if (nch == 3) e = d0x * d0x * s0 - 2.f * d0x * s1 + sk;
+                    else if (nch == 4) e = d0x * d0y * s0 - d0x * s2 - d0y * s1 + sk;
+                    else if (nch == 5) e = d0y * d0y * s0 - 2.f * d0y * s2 + sk;
+                    if (nch < 6) atomicAdd(dst + XW + nch, e);
+                }
+            }
+            wave_lds_sync();
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = (l >> 4) * 4 + i;
@@ -523,7 +557,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         return l < min(NB, hi_b) ? (uint32_t)a.contrib[range.x + (uint32_t)(hi_b - 1 - l)] : 0u;
     };
     int r = 0;
-    if (max_last > 0) issue(batch_gid(max_last), 0);
+    uint32_t gid_cur = max_last > 0 ? batch_gid(max_last) : 0u;  // Gaussian of instance l of the current batch
+    if (max_last > 0) issue(gid_cur, 0);
     uint32_t gid_next = max_last > NB ? batch_gid(max_last - NB) : 0u;
     uint32_t cb_next = max_last > 0 ? batch_bits(max_last) : 0u;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -540,6 +575,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         const long long tm0 = wall_clock64();
 #endif
         const uint32_t cbits = cb_next;
+        const uint32_t gid_staged = gid_next;
         if (hn > 0) {  // block-uniform: stage the next batch while this one blends
             issue(gid_next, buf ^ 1);
             gid_next = hn > NB ? batch_gid(hn - NB) : 0u;
@@ -556,7 +592,9 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         const int lo = hi - wmax;  // instances j < lo lie beyond every pixel of this wave
         if (lo >= NB) bits = 0u;
         else if (lo > 0) bits &= ~(mask_t)0 << lo;
-        if ((bits >> l) & 1u) {
+        if constexpr (ATOM) {
+            row_l = gid_cur;
+        } else if ((bits >> l) & 1u) {
             const uint32_t slot = record_slot(st[NB + l], tx, ty, a.grid_x, a.grid_y);
             row_l = 4 * slot + w;
             a.flags[row_l] = 1;
@@ -603,12 +641,20 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 wr[0] = wv0;
                 wr[GRP * WQS] = qv0;
                 rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j0), r);
+                if constexpr (ATOM) {
+                    d0xr = l == r ? xy0.x - qcx : d0xr;
+                    d0yr = l == r ? xy0.y - qcy : d0yr;
+                }
             }
             if (has1) {
                 float* wr = wq + (r + 1) * WQS + l;
                 wr[0] = wv1;
                 wr[GRP * WQS] = qv1;
                 rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j1), r + 1);
+                if constexpr (ATOM) {
+                    d0xr = l == r + 1 ? xy1.x - qcx : d0xr;
+                    d0yr = l == r + 1 ? xy1.y - qcy : d0yr;
+                }
             }
             r += has1 ? 2 : 1;
             if (r > GRP - 2) {
@@ -627,6 +673,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         t_wait += wall_clock64() - tw0;
 #endif
         buf ^= 1;
+        gid_cur = gid_staged;
     }
     if (r > 0) flush(r);
 #ifdef R3DG_EXP_COUNT
@@ -647,8 +694,10 @@ static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
     const int grid = padded_tile_grid(a.num_tiles);
     if (dpp)
         launch_kernel(render_bwd_dpp_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
+    else if (a.sums_atomic)
+        launch_kernel(render_bwd_glds_kernel<SMAX, true>, dim3(grid), dim3(kBlock), stream, a);
     else
-        launch_kernel(render_bwd_glds_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
+        launch_kernel(render_bwd_glds_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
     return hipGetLastError();
 }
 
@@ -1111,12 +1160,24 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     // sum row -> the kRow layout gather_gaussian reads
     float s[NR];
     if (g < a.g_end) {
-        const float4* src = reinterpret_cast<const float4*>(a.sums + (size_t)g * a.RS);
+        const float4* src = reinterpret_cast<const float4*>(a.sums + (size_t)g * (a.sums_moments ? a.SRS : a.RS));
         float x[XW + 8];
 #pragma unroll
         for (int q = 0; q < XW / 4 + 2; ++q) {
             const float4 v = src[q];
             x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+        }
+        if (a.sums_moments) {
+            // the atomic flush summed the moments about the mean: expand them as row_sum_kernel does
+            const float S0 = x[XW], Sdx = x[XW + 1], Sdy = x[XW + 2], Sdxdx = x[XW + 3], Sdxdy = x[XW + 4],
+                        Sdydy = x[XW + 5];
+            const float4 co = a.conic_opacity[g];
+            x[XW + 0] = -0.5f * a.W * co.w * (co.x * Sdx + co.y * Sdy);
+            x[XW + 1] = -0.5f * a.H * co.w * (co.z * Sdy + co.y * Sdx);
+            x[XW + 2] = -0.5f * co.w * Sdxdx;
+            x[XW + 3] = -0.5f * co.w * Sdxdy;
+            x[XW + 4] = -0.5f * co.w * Sdydy;
+            x[XW + 5] = S0;
         }
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) s[kRowColor + ch] = x[ch];

@@ -218,15 +218,19 @@ render_fwd_shader_kernel(RenderFwdArgs a) {
                          // 128: 24.6 KB -> 6 waves/SIMD, measured 0.480 vs 0.447 ms at M1)
 #endif
 
-template <int SMAX>
+// SHADER (non-default splat shaders, forward.cu:907-971): one more staged column per instance, the
+// splat shaders' colour (RenderFwdArgs::shader_rec), blended into the shader image alongside the SH
+// colour -- the same DMA staging, cull, step and contribution bits as the default path.
+template <int SMAX, bool SHADER>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_FWD_WAVES : 1)))
 render_fwd_glds_kernel(RenderFwdArgs a) {
     constexpr int NB = R3DG_FWDG_NB;
     constexpr int NH = NB / 64;                // staged instances per lane
     constexpr int NA4 = (4 + SMAX + 3) / 4;    // float4 per attribute row
     constexpr int RF4 = 2 + NA4;               // float4 per render record
-    constexpr int SBUF = RF4 * NB;             // float4 per staging buffer
-    constexpr int NCP = RF4 * NH;              // DMA wave-instructions per batch
+    constexpr int NCOL = RF4 + (SHADER ? 1 : 0);  // staged float4 columns per instance
+    constexpr int SBUF = NCOL * NB;            // float4 per staging buffer
+    constexpr int NCP = NCOL * NH;             // DMA wave-instructions per batch
     static_assert(NB == 64, "one 64-bit contribution word per wave and batch");
     // one LDS array: [2 staging buffers | 2 x 64 x 4 contribution flags (batch buffer, instance, wave)
     // | the tile's sorted Gaussian ids (fused sort)]; the fused sort's scratch aliases the staging
@@ -279,6 +283,9 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     float T = 1.0f;
     uint32_t last = 0;
     float C[3] = {0.f, 0.f, 0.f}, F[SMAX > 0 ? SMAX : 1];
+    float CS[SHADER ? 3 : 1];
+#pragma unroll
+    for (int c = 0; c < (SHADER ? 3 : 1); ++c) CS[c] = 0.f;
     float Dp = 0.f, Op = 0.f;
 #pragma unroll
     for (int c = 0; c < SMAX; ++c) F[c] = 0.f;
@@ -300,7 +307,8 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         for (int k = 0; k < NCP; ++k) {
             if ((k & 3) != w) continue;  // wave-uniform
             // lane l of instruction k: column k / NH, instance (k % NH) * 64 + l -> entry k * 64 + l
-            const float4* src = a.records + (size_t)gd[k % NH] * RF4 + k / NH;
+            const float4* src = (SHADER && k / NH == RF4) ? a.shader_rec + gd[k % NH]
+                                                         : a.records + (size_t)gd[k % NH] * RF4 + k / NH;
             const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)((buf * SBUF + k * 64) * 16));
             int keep;
             asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -387,6 +395,12 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 C[0] = __builtin_fmaf(v[0], wgt, C[0]);
                 C[1] = __builtin_fmaf(v[1], wgt, C[1]);
                 C[2] = __builtin_fmaf(v[2], wgt, C[2]);
+                if constexpr (SHADER) {
+                    const float4 sc = st[RF4 * NB + ju];
+                    CS[0] = __builtin_fmaf(sc.x, wgt, CS[0]);
+                    CS[1] = __builtin_fmaf(sc.y, wgt, CS[1]);
+                    CS[2] = __builtin_fmaf(sc.z, wgt, CS[2]);
+                }
 #pragma unroll
                 for (int c2 = 0; c2 < SMAX; ++c2) F[c2] = __builtin_fmaf(v[4 + c2], wgt, F[c2]);
                 Dp = __builtin_fmaf(v[3], wgt, Dp);
@@ -441,10 +455,16 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         a.out_color[3 * pix + 0] = o0;
         a.out_color[3 * pix + 1] = o1;
         a.out_color[3 * pix + 2] = o2;
-        // default splat shader: shader colour == SH colour (splatShader.cu:67-71)
-        a.out_shader_color[3 * pix + 0] = o0;
-        a.out_shader_color[3 * pix + 1] = o1;
-        a.out_shader_color[3 * pix + 2] = o2;
+        if constexpr (SHADER) {
+            a.out_shader_color[3 * pix + 0] = CS[0] + T * b0;
+            a.out_shader_color[3 * pix + 1] = CS[1] + T * b1;
+            a.out_shader_color[3 * pix + 2] = CS[2] + T * b2;
+        } else {
+            // default splat shader: shader colour == SH colour (splatShader.cu:67-71)
+            a.out_shader_color[3 * pix + 0] = o0;
+            a.out_shader_color[3 * pix + 1] = o1;
+            a.out_shader_color[3 * pix + 2] = o2;
+        }
         a.out_depth[pix] = Dp;
         a.out_opacity[pix] = Op;
         if (a.zero_stencil) a.zero_stencil[pix] = 0.f;
@@ -457,10 +477,13 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
 template <int SMAX>
 static hipError_t launch_fwd_s(const RenderFwdArgs& a, bool shader, hipStream_t stream) {
     const int grid = padded_tile_grid(a.num_tiles);
-    if (shader)
+    const char* e = getenv("R3DG_FWD_SHADER");  // "reg": the register-staged shader kernel (A/B only)
+    if (shader && e && e[0] == 'r')
         launch_kernel(render_fwd_shader_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
+    else if (shader)
+        launch_kernel(render_fwd_glds_kernel<SMAX, true>, dim3(grid), dim3(kBlock), stream, a);
     else
-        launch_kernel(render_fwd_glds_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
+        launch_kernel(render_fwd_glds_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
     return hipGetLastError();
 }
 

@@ -257,11 +257,21 @@ def test_backward_precomputed_colors_and_cov(hip_ext):
 
 
 def test_backward_deterministic(hip_ext):
+    """The deterministic reduction (R3DG_BWD_REDUCE=rows: partial rows summed in a fixed order) gives
+    bitwise the same gradients run to run."""
     scene, cam = synthetic.small_scene(P=3000, S=11, seed=2, width=96, height=96)
-    h = hip_forward(hip_ext, scene, cam, S=11)
-    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11)
-    g1 = hip_backward(hip_ext, h, dc, do, dd, df)
-    g2 = hip_backward(hip_ext, h, dc, do, dd, df)
+    prev = os.environ.get("R3DG_BWD_REDUCE")
+    os.environ["R3DG_BWD_REDUCE"] = "rows"
+    try:
+        h = hip_forward(hip_ext, scene, cam, S=11)
+        dc, do, dd, df = upstream_grads(cam.height, cam.width, 11)
+        g1 = hip_backward(hip_ext, h, dc, do, dd, df)
+        g2 = hip_backward(hip_ext, h, dc, do, dd, df)
+    finally:
+        if prev is None:
+            del os.environ["R3DG_BWD_REDUCE"]
+        else:
+            os.environ["R3DG_BWD_REDUCE"] = prev
     for k in g1:
         np.testing.assert_array_equal(g1[k], g2[k], err_msg=k)
 
@@ -585,6 +595,34 @@ def test_autograd_wrapper(hip_ext):
     assert_close("scales.grad", scales.grad.cpu().numpy(), go["dL_dscales"], _grad_tol(go["dL_dscales"]), 2e-3)
     assert_close("rotations.grad", rots.grad.cpu().numpy(), go["dL_drotations"], _grad_tol(go["dL_drotations"]),
                  2e-3)
+
+
+@pytest.mark.parametrize("reduce", ["atomic", "rows"])
+@pytest.mark.parametrize("S", [0, 11, 21, 32])
+def test_backward_reductions_match_oracle(hip_ext, S, reduce):
+    """Both second stages of the backward's reduction (R3DG_BWD_REDUCE): the per-(instance, wave)
+    rows added straight into the per-Gaussian sums with f32 atomics, and the deterministic partial
+    rows + row_sum_kernel, against the oracle; and against each other."""
+    scene, cam = synthetic.small_scene(P=3000, S=max(S, 21), seed=60 + S, width=112, height=80)
+    o = _oracle_fwd(scene, cam, S)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, S, seed=3)
+    go = oracle.rasterize_backward(o, dc, do, dd, df)
+    prev = os.environ.get("R3DG_BWD_REDUCE")
+    os.environ["R3DG_BWD_REDUCE"] = reduce
+    try:
+        gh = hip_backward(hip_ext, hip_forward(hip_ext, scene, cam, S=S), dc, do, dd, df)
+        os.environ["R3DG_BWD_REDUCE"] = "rows" if reduce == "atomic" else "atomic"
+        gx = hip_backward(hip_ext, hip_forward(hip_ext, scene, cam, S=S), dc, do, dd, df)
+    finally:
+        if prev is None:
+            del os.environ["R3DG_BWD_REDUCE"]
+        else:
+            os.environ["R3DG_BWD_REDUCE"] = prev
+    for k in go:
+        if k in gh:
+            assert_close(f"{reduce} {k}", gh[k], go[k], _grad_tol(go[k]), 2e-3)
+            assert_close(f"{reduce} vs other {k}", gh[k], gx[k], 1e-6 * max(float(np.abs(gx[k]).max()) if gx[k].size
+                                                                           else 0.0, 1e-12), 1e-4)
 
 
 @pytest.mark.parametrize("S", [11, 21])
