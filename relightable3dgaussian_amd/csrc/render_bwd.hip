@@ -827,6 +827,7 @@ __device__ static void cov3d_backward(float3 sc, float mod, float4 q, const floa
 // summed row, `shl` this Gaussian's SH coefficients in LDS, replaced by dL/dsh on return.
 template <int SMAX>
 __device__ __forceinline__ void gather_gaussian(const GatherBwdArgs& a, int g, const float* s, float* shl) {
+#pragma clang fp contract(off)  // the oracle's operation sequence (cov2D backward is ill-conditioned)
     a.dL_dmeans2D[3 * g + 0] = s[kRowMean + 0];
     a.dL_dmeans2D[3 * g + 1] = s[kRowMean + 1];
     a.dL_dmeans2D[3 * g + 2] = s[kRowMean + 2];
