@@ -265,19 +265,61 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// x = h + m + o to within 2^-24 |x|: three bf16 terms, each the round-to-nearest of what the
-// previous ones left (the differences are exact in f32), so h*y + m*y + o*y with y exact in bf16
-// (the pixel moments 1, x, y, x^2, xy, y^2 of half-integer offsets are) gives the f32 product.
+// Exact bf16 splits by truncation: h = the top 8 significant bits of x (its upper 16 bits), r = x - h
+// exact in f32 (<= 16 significant bits), m = the top 8 significant bits of r, o = r - m exact and
+// <= 8 significant bits, so x = h + m + o EXACTLY and h*y + m*y + o*y with y exact in bf16 (the
+// pixel moments 1, x, y, x^2, xy, y^2 of half-integer offsets are) gives the f32 product. Per value
+// two v_and + two v_sub, and per value pair one v_perm_b32 per term packing the two upper halves
+// (round-to-nearest conversions cost 3.5 v_cvt_pk_bf16_f32 + 2 shifts + 2 subs per value).
+union bf16x8_u {
+    bf16x8 v;
+    uint32_t u[4];
+};
+__device__ __forceinline__ uint32_t hi16_pair(uint32_t lo, uint32_t hi) {
+    return __builtin_amdgcn_perm(hi, lo, 0x07060302u);  // [lo.upper16 | hi.upper16]
+}
 __device__ __forceinline__ void split_bf16x3(const float (&x)[8], bf16x8& h, bf16x8& m, bf16x8& o) {
+    uint32_t ux[8], ur[8], uo[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const __bf16 hb = (__bf16)x[i];
-        const float r = x[i] - (float)hb;
-        const __bf16 mb = (__bf16)r;
-        h[i] = hb;
-        m[i] = mb;
-        o[i] = (__bf16)(r - (float)mb);
+        ux[i] = __float_as_uint(x[i]);
+        const float r = x[i] - __uint_as_float(ux[i] & 0xffff0000u);
+        ur[i] = __float_as_uint(r);
+        uo[i] = __float_as_uint(r - __uint_as_float(ur[i] & 0xffff0000u));
     }
+    bf16x8_u H, M, O;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        H.u[k] = hi16_pair(ux[2 * k], ux[2 * k + 1]);
+        M.u[k] = hi16_pair(ur[2 * k], ur[2 * k + 1]);
+        O.u[k] = hi16_pair(uo[2 * k], uo[2 * k + 1]);
+    }
+    h = H.v;
+    m = M.v;
+    o = O.v;
+}
+
+#ifndef R3DG_BWD_SPLIT
+#define R3DG_BWD_SPLIT 3  // bf16 terms per f32 value in the flush's MFMA products: 3 = exact f32
+                          // products; 2 = two-term splits (relative error < 2^-15 per product)
+#endif
+
+// x = h + m to within 2^-15 |x| (two-term form of split_bf16x3)
+__device__ __forceinline__ void split_bf16x2(const float (&x)[8], bf16x8& h, bf16x8& m) {
+    uint32_t ux[8], ur[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        ux[i] = __float_as_uint(x[i]);
+        ur[i] = __float_as_uint(x[i] - __uint_as_float(ux[i] & 0xffff0000u));
+    }
+    bf16x8_u H, M;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        H.u[k] = hi16_pair(ux[2 * k], ux[2 * k + 1]);
+        M.u[k] = hi16_pair(ur[2 * k], ur[2 * k + 1]);
+    }
+    h = H.v;
+    m = M.v;
 }
 
 #ifndef R3DG_BWDG_NB
@@ -456,6 +498,16 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) wv[i] = src[i];
             bf16x8 h, m, o;
+#if R3DG_BWD_SPLIT == 2
+            split_bf16x2(wv, h, m);
+            (void)o;
+#pragma unroll
+            for (int xb = 0; xb < NXB; ++xb) {
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bXh[xb][b], accX[xb], 0, 0, 0);
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXl[xb][b], accX[xb], 0, 0, 0);
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
+            }
+#else
             split_bf16x3(wv, h, m, o);
 #pragma unroll
             for (int xb = 0; xb < NXB; ++xb) {
@@ -465,6 +517,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXl[xb][b], accX[xb], 0, 0, 0);
                 accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
             }
+#endif
         }
         // q rows times the moments on the bf16 MFMA (16 cycles per K = 32, against 32 per K = 4 in
         // f32): three exact-sum bf16 terms of q per K-block
@@ -475,10 +528,17 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) qv[i] = src[i];
             bf16x8 h, m, o;
+#if R3DG_BWD_SPLIT == 2
+            split_bf16x2(qv, h, m);
+            (void)o;
+            accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, yb[b], accY, 0, 0, 0);
+            accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, yb[b], accY, 0, 0, 0);
+#else
             split_bf16x3(qv, h, m, o);
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, yb[b], accY, 0, 0, 0);
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, yb[b], accY, 0, 0, 0);
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o, yb[b], accY, 0, 0, 0);
+#endif
         }
         if constexpr (ATOM) {
 #pragma unroll

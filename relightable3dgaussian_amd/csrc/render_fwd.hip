@@ -267,7 +267,9 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
             keys[k] = kv.x;
             vals[k] = kv.y;
         }
+#ifndef R3DG_EXP_NOSORT  // timing experiment only (results invalid): the blend without the fused sort
         if (n > 1) sort_pairs_chunk<IPT>(keys, vals, n, *reinterpret_cast<TileSortLds<IPT>*>(s_lds));
+#endif
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const int i = t * IPT + k;
