@@ -213,6 +213,10 @@ render_fwd_shader_kernel(RenderFwdArgs a) {
 // own quadrant. Staging layout: column q (float4 q of the render record) of instance j at
 // [q * NB + j]. Same blend step, same decisions and sums as render_fwd_shader_kernel (bitwise).
 // ---------------------------------------------------------------------------------------------
+#ifndef R3DG_FWD_BITONIC
+#define R3DG_FWD_BITONIC 0  // fused sort: 1 = bitonic network (r3dg_tilesort.h), 0 = rocPRIM radix passes
+#endif
+
 #ifndef R3DG_FWDG_NB
 #define R3DG_FWDG_NB 64  // instances per staged batch (two resident: 12.3 KB, 64 VGPRs -> 8 waves/SIMD;
                          // 128: 24.6 KB -> 6 waves/SIMD, measured 0.480 vs 0.447 ms at M1)
@@ -234,7 +238,9 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     static_assert(NB == 64, "one 64-bit contribution word per wave and batch");
     // one LDS array: [2 staging buffers | 2 x 64 x 4 contribution flags (batch buffer, instance, wave)
     // | the tile's sorted Gaussian ids (fused sort)]; the fused sort's scratch aliases the staging
-    constexpr int SORT4 = (int)((sizeof(TileSortLds<kFusedSortMax / kSortBT>) + 15) / 16);
+    constexpr int SORT4a = (int)((sizeof(TileSortLds<kFusedSortMax / kSortBT>) + 15) / 16);
+    constexpr int SORT4b = 2 * kFusedSortMax / 4;              // bitonic_sort_pairs' key / value scratch
+    constexpr int SORT4 = SORT4a > SORT4b ? SORT4a : SORT4b;
     constexpr int STG = 2 * SBUF > SORT4 ? 2 * SBUF : SORT4;  // float4 of staging / sort scratch
     __shared__ float4 s_lds[STG + 32 + kFusedSortMax / 4];
     uint8_t* const s_cf = reinterpret_cast<uint8_t*>(s_lds + STG);
@@ -268,7 +274,11 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
             vals[k] = kv.y;
         }
 #ifndef R3DG_EXP_NOSORT  // timing experiment only (results invalid): the blend without the fused sort
+#if R3DG_FWD_BITONIC
+        if (n > 1) bitonic_sort_pairs<IPT>(keys, vals, n, reinterpret_cast<uint32_t*>(s_lds));
+#else
         if (n > 1) sort_pairs_chunk<IPT>(keys, vals, n, *reinterpret_cast<TileSortLds<IPT>*>(s_lds));
+#endif
 #endif
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
