@@ -11,7 +11,7 @@ for spec in "$@"; do
   if [[ "$spec" == *+* ]]; then envs=${spec#*+}; fi
   n=$(echo "$spec" | tr '+=,/' '__._')
   (for kv in ${envs//,/ }; do export "$kv"; done
-   timeout -k 10 150 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/$n.json 2> $OUT/$n.err) \
+   timeout -k 10 150 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/$n.json 2> $OUT/$n.err) \
     || { tail -20 $OUT/$n.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/$n.json')); print('$spec', d['ms_per_step'], d['kernel_ms'], d['roofline']['frac'])"
 done
