@@ -393,10 +393,11 @@ def main() -> None:
     bf, bb = algorithmic_bytes(L, npix, tiles, S_M1)
     # per-step device time of each stage
     avg = {k: v[1] / args.steps for k, v in prof.items()}
-    launch = {k: (v[1] / v[0] if v[0] else float("nan")) for k, v in prof.items()}
+    launch = {k: (v[1] / v[0] if v[0] else 0.0) for k, v in prof.items()}
     # renderCUDA fwd + bwd: the backward blend AND its per-instance reduction (row_sum_kernel sums
     # the partial rows the reference accumulates with atomics, backward.cu:552-611)
-    t_kern = (launch["render_fwd"] + launch["render_bwd"] + launch.get("row_sum", 0.0)) / 1e3
+    # (with the atomic flush, R3DG_BWD_REDUCE=atomic, the row_sum slot times the sums' zeroing)
+    t_kern = (launch["render_fwd"] + launch["render_bwd"] + launch["row_sum"]) / 1e3
     achieved = (bf + bb) / t_kern / 1e9
     traffic = None
     tr = load_traffic()

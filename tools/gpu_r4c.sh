@@ -12,5 +12,5 @@ R3DG_LIB_DIR=exp/BITONIC/lib timeout -k 10 400 python -u -m pytest tests/test_gp
   -k "keys or sort or dense or binning or forward" --timeout 200 --timeout-method thread > $OUT/bitonic.log 2>&1 \
   || { tail -30 $OUT/bitonic.log; exit 1; }
 tail -1 $OUT/bitonic.log
-bash tools/gpu_ab_env.sh r4c base base+R3DG_BWD_REDUCE=atomic rne+R3DG_LIB_DIR=exp/RNE/lib split2+R3DG_LIB_DIR=exp/SPLIT2/lib split2a+R3DG_LIB_DIR=exp/SPLIT2/lib,R3DG_BWD_REDUCE=atomic nosort+R3DG_LIB_DIR=exp/NOSORT/lib bitonic+R3DG_LIB_DIR=exp/BITONIC/lib base.2 base+R3DG_BWD_REDUCE=atomic.2 rne.2+R3DG_LIB_DIR=exp/RNE/lib bitonic.2+R3DG_LIB_DIR=exp/BITONIC/lib
+bash tools/gpu_ab_env.sh r4c base base+R3DG_BWD_REDUCE=atomic,R3DG_BWD_SRS=24 base+R3DG_BWD_REDUCE=atomic rne+R3DG_LIB_DIR=exp/RNE/lib split2+R3DG_LIB_DIR=exp/SPLIT2/lib split2a+R3DG_LIB_DIR=exp/SPLIT2/lib,R3DG_BWD_REDUCE=atomic nosort+R3DG_LIB_DIR=exp/NOSORT/lib bitonic+R3DG_LIB_DIR=exp/BITONIC/lib base.2 base+R3DG_BWD_REDUCE=atomic.2 rne.2+R3DG_LIB_DIR=exp/RNE/lib bitonic.2+R3DG_LIB_DIR=exp/BITONIC/lib
 BENCH_ARGS="--P 2000000" bash tools/gpu_ab_env.sh r4c_c4 base bitonic+R3DG_LIB_DIR=exp/BITONIC/lib base.2 bitonic.2+R3DG_LIB_DIR=exp/BITONIC/lib

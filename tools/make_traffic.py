@@ -15,7 +15,7 @@ def pick(prefix):
     for k, v in d.items():
         if k.startswith(prefix):
             return k, v
-    raise KeyError(prefix)
+    return None, None  # a kernel the build no longer launches (row_sum_kernel with the atomic flush)
 
 
 out = {"config": config, "source": src, "method": "FETCH_SIZE*2 + WRITE_SIZE (KiB*1024), mean per launch"}
@@ -23,6 +23,8 @@ for name, prefix in [("render_fwd", "render_fwd_glds_kernel"), ("render_bwd", "r
                      ("row_sum", "row_sum_kernel"), ("gather_bwd", "gather_bwd_kernel"),
                      ("preprocess", "preprocess_kernel")]:
     k, v = pick(prefix)
+    if k is None:
+        continue
     out[name + "_kernel"] = k
     out[name + "_bytes"] = int(round((2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024))
 json.dump(out, open(dst, "w"), indent=1)

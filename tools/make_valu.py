@@ -27,7 +27,7 @@ def pick(prefix):
     for k, v in d.items():
         if k.startswith(prefix):
             return k, v
-    raise KeyError(prefix)
+    return None, None  # a kernel the build no longer launches (row_sum_kernel with the atomic flush)
 
 
 out = {"config": config, "source": [pmc, cnt],
@@ -39,6 +39,8 @@ steps = {k: (v // runs if v else v) for k, v in
 for name, prefix in [("render_fwd", "render_fwd_glds_kernel"), ("render_bwd", "render_bwd_glds_kernel"),
                      ("row_sum", "row_sum_kernel")]:
     k, v = pick(prefix)
+    if k is None:
+        continue
     ent = {"kernel": k, "valu_insts": int(round(v["SQ_INSTS_VALU"] - v.get("SQ_INSTS_MFMA", 0.0))),
            "mfma_insts": int(round(v.get("SQ_INSTS_MFMA", 0.0))), "salu_insts": int(round(v.get("SQ_INSTS_SALU", 0)))}
     if steps.get(name):
