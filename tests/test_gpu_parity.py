@@ -182,14 +182,14 @@ def test_cull_exact_needles(hip_ext):
     # dL/dcov3D and the cov2D part of dL/dmeans3D go through the conic inverse (backward.cu:
     # 180-230): with cov2D ~ [[5e5, +-5e5], [+-5e5, 5e5]] its determinant is a ~1e6-fold cancellation
     # of a*c against b^2 in fp32, so an fp32 rounding of dL/dconic moves them by O(1). Their bar is
-    # the problem's own sensitivity: the oracle run again on upstream gradients perturbed by one
-    # rounding (x (1 +- 2^-24), two draws) spreads by s per Gaussian; the GPU must lie within
+    # the problem's own sensitivity: the oracle run again on upstream gradients moved by one ulp
+    # each (random direction, three draws) spreads by s per Gaussian; the GPU must lie within
     # 4 * max(s) of the oracle per Gaussian (+ 2e-5 of the largest gradient).
     rng = np.random.default_rng(99)
     spread = {k: np.zeros(gh[k].shape[0]) for k in ["dL_dmeans3D", "dL_dcov3D", "dL_dscales", "dL_drotations"]}
-    for _ in range(2):
-        pert = [(x * (1.0 + rng.choice([-1.0, 1.0], size=x.shape) * 2.0 ** -24)).astype(np.float32)
-                for x in (dc, do, dd, df)]
+    for _ in range(3):
+        pert = [np.nextafter(x, np.where(rng.random(x.shape) < 0.5, -np.inf, np.inf).astype(np.float32))
+                .astype(np.float32) for x in (dc, do, dd, df)]
         gp = oracle.rasterize_backward(o, *pert)
         for k in spread:
             d = np.abs(gp[k].astype(np.float64) - go[k]).reshape(go[k].shape[0], -1).max(1)
