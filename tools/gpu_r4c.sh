@@ -5,7 +5,7 @@ set -e
 OUT=gpurun_out/r4c
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_shaders.py tests/test_postprocess.py -m gpu -x -q -s \
-  -k "brdf or reductions or shader or splat or post or texture or needles" --timeout 200 --timeout-method thread > $OUT/parity.log 2>&1 \
+  -k "brdf or reductions or shader or splat or post or texture" --timeout 200 --timeout-method thread > $OUT/parity.log 2>&1 \
   || { grep -h "brdf \|passed\|failed\|Error\|assert" $OUT/parity.log | tail -40; exit 1; }
 grep -h "brdf \|passed\|failed" $OUT/parity.log | tail -40
 R3DG_LIB_DIR=exp/BITONIC/lib timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q \
