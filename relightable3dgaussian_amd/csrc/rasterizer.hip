@@ -229,17 +229,22 @@ __global__ void __launch_bounds__(256) init_stencil_kernel(int P, float* stencil
 
 // Splat shaders edit conic_opacity.w after the render records were written: refresh the records'
 // opacity (the backward reads records; the reference's backward reads the edited geometry state).
-// Also packs the splat shaders' colour into one float4 per Gaussian, the shader blend's extra
-// staged record column (render_fwd_glds_kernel<SMAX, true>).
+// Also writes the shader record of every visible Gaussian (render_fwd_glds_kernel<SMAX, true>):
+// rec4 - 2 float4 in the attribute row's layout, [shader colour, 0 | the splat shaders' features,
+// zero padded] -- the blend's staged colour and feature columns after the splat shaders ran.
 __global__ void __launch_bounds__(256) refresh_record_opacity_kernel(int P, const int* __restrict__ radii,
                                                                      const float4* __restrict__ conic_opacity,
                                                                      float4* __restrict__ records, int rec4,
                                                                      const float* __restrict__ shader_rgb,
-                                                                     float4* __restrict__ shader_rec) {
+                                                                     const float* __restrict__ feats, int S,
+                                                                     float* __restrict__ shader_rec) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P || radii[i] <= 0) return;
     records[(size_t)i * rec4].w = conic_opacity[i].w;
-    shader_rec[i] = make_float4(shader_rgb[3 * i], shader_rgb[3 * i + 1], shader_rgb[3 * i + 2], 0.f);
+    const int nf = 4 * (rec4 - 2);
+    float* o = shader_rec + (size_t)i * nf;
+    o[0] = shader_rgb[3 * i]; o[1] = shader_rgb[3 * i + 1]; o[2] = shader_rgb[3 * i + 2]; o[3] = 0.f;
+    for (int c = 4; c < nf; ++c) o[c] = c - 4 < S ? feats[(size_t)i * S + (c - 4)] : 0.f;
 }
 
 // ---- shader registry (ShShader.cu:196-230, splatShader.cu:283-333, postProcessShader.cu:395-436) ----
@@ -483,7 +488,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     const size_t post_floats = post_blur ? (size_t)3 * H * W : 0;  // BlurLighting's incident-light snapshot
     // the splat shaders' colour as one float4 per Gaussian (16-B aligned, after the other extras)
     const size_t shrec_off = (work_floats + post_floats + 3) & ~(size_t)3;
-    const size_t shrec_floats = splat_active ? 4 * (size_t)P : 0;
+    const size_t shrec_floats = splat_active ? 4 * (size_t)P * (record_f4(S) - 2) : 0;
     void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * (shrec_off + shrec_floats));
     // with a scratch allocator the binning's tile counts are transient (needed only until the
     // scatter), not part of the image state autograd keeps alive until the backward
@@ -549,6 +554,10 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         }
     }
 
+    // the default-shader blend sorts its tiles itself (fused, tiles of up to kFusedSortMax instances)
+    // only for S <= 12: with more feature channels its registers leave fewer waves to hide the
+    // sort's barriers (M1 with S = 21: fused blend 0.78 ms vs 0.49 + 0.10 ms for the separate sort)
+    const bool fuse_sort = !splat_active && S <= 12;
     int L = 0;
     BinArgs binning{};
     binning.P = P; binning.grid_x = gx; binning.grid_y = gy; binning.rec4 = record_f4(S); binning.T = T;
@@ -643,7 +652,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         // the default-shader blend sorts the tiles of up to kFusedSortMax instances itself
         R3DG_CHECK_HIP(launch_tile_depth_sort(T, img.ranges, img.tile_order, bin.pairs, bin.point_list,
                                               bin.sort_k1, bin.sort_v1, bin.sort_k2,
-                                              splat_active ? 0 : kFusedSortMax, st));
+                                              fuse_sort ? kFusedSortMax : 0, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
@@ -673,7 +682,8 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
             R3DG_CHECK_LAUNCH(s->debug, st);
         }
         hipLaunchKernelGGL(refresh_record_opacity_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, radii,
-                           geom.conic_opacity, geom.records, record_f4(S), geom.shader_rgb, shader_rec);
+                           geom.conic_opacity, geom.records, record_f4(S), geom.shader_rgb, feats, S,
+                           reinterpret_cast<float*>(shader_rec));
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
@@ -702,7 +712,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     // the blend writes those zeros with its other outputs (no separate memset launch)
     ra.zero_stencil = splat_active ? nullptr : out->stencil;
     ra.contrib = bin.contrib;
-    ra.pairs = splat_active ? nullptr : bin.pairs;  // fused depth sort (render_fwd_glds_kernel)
+    ra.pairs = fuse_sort ? bin.pairs : nullptr;  // fused depth sort (render_fwd_glds_kernel)
     ra.point_list_out = bin.point_list;
     ra.shader_rec = shader_rec;
     if (const char* e = getenv("R3DG_NO_CULL")) ra.cull = (e[0] == '0');

@@ -222,9 +222,12 @@ render_fwd_shader_kernel(RenderFwdArgs a) {
                          // 128: 24.6 KB -> 6 waves/SIMD, measured 0.480 vs 0.447 ms at M1)
 #endif
 
-// SHADER (non-default splat shaders, forward.cu:907-971): one more staged column per instance, the
-// splat shaders' colour (RenderFwdArgs::shader_rec), blended into the shader image alongside the SH
-// colour -- the same DMA staging, cull, step and contribution bits as the default path.
+// SHADER (non-default splat shaders, forward.cu:907-971): the splat shaders edit the shader colour
+// and the features after the render records were written (the records keep the caller's features:
+// the backward reads those, as the reference's does), so the staged columns are the record's conic,
+// position and [colour, depth] float4 followed by the shader record [shader colour, 0 | shaded
+// features] (RenderFwdArgs::shader_rec, NA4 float4 per Gaussian, the attribute row's layout) -- the
+// same DMA staging, cull, step and contribution bits as the default path.
 template <int SMAX, bool SHADER>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_FWD_WAVES : 1)))
 render_fwd_glds_kernel(RenderFwdArgs a) {
@@ -232,7 +235,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     constexpr int NH = NB / 64;                // staged instances per lane
     constexpr int NA4 = (4 + SMAX + 3) / 4;    // float4 per attribute row
     constexpr int RF4 = 2 + NA4;               // float4 per render record
-    constexpr int NCOL = RF4 + (SHADER ? 1 : 0);  // staged float4 columns per instance
+    constexpr int NCOL = RF4 + (SHADER ? 1 : 0);  // staged float4 columns per instance (SHADER: 3 + NA4)
     constexpr int SBUF = NCOL * NB;            // float4 per staging buffer
     constexpr int NCP = NCOL * NH;             // DMA wave-instructions per batch
     static_assert(NB == 64, "one 64-bit contribution word per wave and batch");
@@ -319,8 +322,8 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         for (int k = 0; k < NCP; ++k) {
             if ((k & 3) != w) continue;  // wave-uniform
             // lane l of instruction k: column k / NH, instance (k % NH) * 64 + l -> entry k * 64 + l
-            const float4* src = (SHADER && k / NH == RF4) ? a.shader_rec + gd[k % NH]
-                                                         : a.records + (size_t)gd[k % NH] * RF4 + k / NH;
+            const float4* src = (SHADER && k / NH >= 3) ? a.shader_rec + (size_t)gd[k % NH] * NA4 + (k / NH - 3)
+                                                       : a.records + (size_t)gd[k % NH] * RF4 + k / NH;
             const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)((buf * SBUF + k * 64) * 16));
             int keep;
             asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -385,7 +388,8 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
             float v[NA4 * 4];
 #pragma unroll
             for (int q = 0; q < NA4; ++q) {
-                const float4 r = st[(2 + q) * NB + ju];
+                // SHADER: [colour, depth] from the record, the shaded features from the shader record
+                const float4 r = st[((SHADER && q > 0) ? 3 + q : 2 + q) * NB + ju];
                 v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
             }
             const float alpha = fminf(0.99f, opacity * G);  // bit-identical to the oracle
@@ -408,7 +412,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 C[1] = __builtin_fmaf(v[1], wgt, C[1]);
                 C[2] = __builtin_fmaf(v[2], wgt, C[2]);
                 if constexpr (SHADER) {
-                    const float4 sc = st[RF4 * NB + ju];
+                    const float4 sc = st[3 * NB + ju];
                     CS[0] = __builtin_fmaf(sc.x, wgt, CS[0]);
                     CS[1] = __builtin_fmaf(sc.y, wgt, CS[1]);
                     CS[2] = __builtin_fmaf(sc.z, wgt, CS[2]);

@@ -21,7 +21,7 @@ for s in $STEPS; do
       timeout -k 10 200 python bench.py --no-cpu-baseline > $OUT/benchq.json 2> $OUT/benchq.err || { tail -20 $OUT/benchq.err; exit 1; }
       python -c "import json; d=json.load(open('$OUT/benchq.json')); print(d['value'], d['ms_per_step'], d['kernel_ms'], d['roofline']['frac'])" ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1 \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof.log 2>&1 \
         || { tail -20 $OUT/prof.log; exit 1; }
       f=$(find $OUT/prof -name '*kernel_stats.csv' | head -1); cp "$f" $OUT/kernel_stats.csv; head -12 $OUT/kernel_stats.csv | cut -c1-160 ;;
   esac
