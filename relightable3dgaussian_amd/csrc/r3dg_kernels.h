@@ -199,6 +199,9 @@ struct IntermediateArgs {
     int W, H, grid_x, num_tiles;
     float* out_depth;
     float* out_stencil;
+    const float4* records;  // render records (intermediate_glds_kernel stages conic + opacity, position)
+    int rec4;
+    float4* inter_rec;      // [P] scratch: [depth, stencil, stencil opacity, 0], packed per launch
 };
 
 // kernels (defined in the .hip translation units)
@@ -229,6 +232,8 @@ __device__ __forceinline__ uint32_t instance_slot(const uint32_t* offsets, float
 }
 __global__ void xyz_normal_kernel(XyzNormalArgs a);
 __global__ void intermediate_kernel(IntermediateArgs a);
+// RenderIntermediateTextures: packs the per-Gaussian depth / stencil record, then the DMA-staged blend
+hipError_t launch_intermediate(const IntermediateArgs& a, int P, const int* radii, hipStream_t st);
 
 // host launchers for the templated blend kernels
 hipError_t launch_render_forward(const RenderFwdArgs& a, bool shader, hipStream_t stream);

@@ -489,7 +489,9 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     // the splat shaders' colour as one float4 per Gaussian (16-B aligned, after the other extras)
     const size_t shrec_off = (work_floats + post_floats + 3) & ~(size_t)3;
     const size_t shrec_floats = splat_active ? 4 * (size_t)P * (record_f4(S) - 2) : 0;
-    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * (shrec_off + shrec_floats));
+    // the intermediate depth / stencil pass's packed per-Gaussian record (launch_intermediate)
+    const size_t inter_floats = (splat_active || !post_ids.empty()) ? 4 * (size_t)P : 0;
+    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * (shrec_off + shrec_floats + inter_floats));
     // with a scratch allocator the binning's tile counts are transient (needed only until the
     // scatter), not part of the image state autograd keeps alive until the backward
     const bool hist_scratch = scratch_alloc != nullptr && P > 0;
@@ -503,6 +505,9 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     float4* shader_rec =
         splat_active ? reinterpret_cast<float4*>(static_cast<char*>(geom_base) + geom_bytes + sizeof(float) * shrec_off)
                      : nullptr;
+    float4* inter_rec = inter_floats ? reinterpret_cast<float4*>(static_cast<char*>(geom_base) + geom_bytes +
+                                                                 sizeof(float) * (shrec_off + shrec_floats))
+                                     : nullptr;
     ImageState img = carve_image((uintptr_t)img_base, H, W, nullptr, !hist_scratch);
     if (hist_scratch) img.bin_hist = hist_base;
     int* radii = out->radii ? out->radii : geom.internal_radii;
@@ -662,10 +667,11 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     ia.conic_opacity = geom.conic_opacity; ia.depths = geom.depths; ia.stencils = geom.stencils;
     ia.stencil_opacity = geom.stencil_opacity; ia.W = W; ia.H = H; ia.grid_x = gx; ia.num_tiles = T;
     ia.out_depth = out->depth; ia.out_stencil = out->stencil;
+    ia.records = geom.records; ia.rec4 = record_f4(S); ia.inter_rec = inter_rec;
     if (splat_active) {
         // the splat shaders read the intermediate depth / stencil images
         R3DG_REQUIRE(out->depth && out->stencil, "rasterize_gaussians: splat shaders need depth and stencil outputs");
-        hipLaunchKernelGGL(intermediate_kernel, dim3(padded_tile_grid(T)), dim3(kBlock), 0, st, ia);
+        R3DG_CHECK_HIP(launch_intermediate(ia, P, radii, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
         for (int id = 0; id < (int)spm->counts.size(); ++id) {  // RunSplatShaders (forward.cu:907-971)
             if (spm->counts[id] == 0) continue;
@@ -737,7 +743,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     if (!post_ids.empty()) {
         // rasterizer_impl.cu:485-529: depth and stencil are rendered again (now with the splat
         // shaders' stencils) and replace the blended depth, then the passes run in list order
-        hipLaunchKernelGGL(intermediate_kernel, dim3(padded_tile_grid(T)), dim3(kBlock), 0, st, ia);
+        R3DG_CHECK_HIP(launch_intermediate(ia, P, radii, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
         PostArgs pp{};
         pp.W = W; pp.H = H; pp.sh_color = out->color; pp.opacity = out->opacity; pp.depth = out->depth;

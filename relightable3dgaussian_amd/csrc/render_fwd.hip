@@ -514,6 +514,137 @@ hipError_t launch_render_forward(const RenderFwdArgs& a, bool shader, hipStream_
     return launch_fwd_s<32>(a, shader, stream);
 }
 
+// forward.cu:271-383 (RenderIntermediateTexturesCUDA) on the default blend's machinery: the
+// render record's conic + opacity and position plus one packed float4 [depth, stencil,
+// stencil opacity, 0] per Gaussian (IntermediateArgs::inter_rec, packed by the caller right before
+// the launch: the splat shaders edit stencils) are copied HBM -> LDS by LDS-DMA one 64-instance batch
+// ahead; each wave culls the staged instances for its 8x8 quadrant with the larger of the two
+// opacities (an instance it skips fails both alpha tests on every pixel of the quadrant) and
+// steps through the survivors two at a time (both exps packed). The arithmetic is the oracle's
+// (oracle_render_intermediate: contraction off, plain products), the Stencil accumulator starts
+// at 0 (the reference leaves it uninitialised, forward.cu:312). Replaces the register-staged
+// 256-instance kernel below, which evaluated every (instance, pixel) pair of the tile list.
+__global__ void __launch_bounds__(kBlock) intermediate_glds_kernel(IntermediateArgs a) {
+#pragma clang fp contract(off)
+    constexpr int NB = 64, NCOL = 3, SBUF = NCOL * NB;
+    __shared__ float4 s_lds[2 * SBUF];
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (tile >= a.num_tiles) return;
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
+    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const float pfx = (float)px, pfy = (float)py;
+    const float qx0 = (float)(tx * kTileX + (w & 1) * 8), qy0 = (float)(ty * kTileY + (w >> 1) * 8);
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+    bool done = !inside;
+    float sT = 1.f, T = 1.f, St = 0.f, Dp = 0.f;
+
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)s_lds;
+    auto gid_of = [&](int b0) { return a.point_list[range.x + (uint32_t)min(b0 + l, n - 1)]; };
+    auto issue = [&](uint32_t gid, int buf) {
+#pragma unroll
+        for (int k = 0; k < NCOL; ++k) {
+            if ((k & 3) != w) continue;  // wave-uniform
+            const float4* src = k < 2 ? a.records + (size_t)gid * a.rec4 + k : a.inter_rec + gid;
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)((buf * SBUF + k * NB) * 16));
+            int keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+        }
+    };
+    uint32_t gnext = 0;
+    if (n > 0) {
+        issue(gid_of(0), 0);
+        if (n > NB) gnext = gid_of(NB);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int buf = 0;
+    for (int base = 0; base < n; base += NB) {
+        if (__syncthreads_count(done) == kBlock) break;
+        if (base + NB < n) {  // block-uniform: stage the next batch while this one blends
+            issue(gnext, buf ^ 1);
+            if (base + 2 * NB < n) gnext = gid_of(base + 2 * NB);
+        }
+        const float4* st = s_lds + buf * SBUF;
+        const int cnt = min(NB, n - base);
+        bool mine = false;
+        if (l < cnt) {
+            float4 co = st[l];
+            const float4 r1 = st[NB + l];
+            co.w = fmaxf(co.w, st[2 * NB + l].z);  // either alpha may pass
+            mine = quadrant_live(make_float2(r1.x, r1.y), co, qx0, qy0, 1);
+        }
+        unsigned long long bits = __ballot(mine);
+        auto step = [&](int j, bool live, float power, float G) {
+            const int ju = __builtin_amdgcn_readfirstlane(j);
+            const float o = st[ju].w;
+            const float4 ds = st[2 * NB + ju];  // depth, stencil, stencil opacity
+            const float alpha = fminf(0.99f, o * G), salpha = fminf(0.99f, ds.z * G);
+            if (!live || done || power > 0.0f || (alpha < 1.0f / 255.0f && salpha < 1.0f / 255.0f)) return;
+            const float tT = T * (1 - alpha), tS = sT * (1 - salpha);
+            if (tT < 0.0001f && tS < 0.0001f) {
+                done = true;
+                return;
+            }
+            Dp += ds.x * (alpha * T);
+            T = tT;
+            St += ds.y * (salpha * sT);
+            sT = tS;
+        };
+        while (bits && __ballot(!done) != 0ull) {
+            const int j0 = (int)__builtin_ctzll(bits);
+            bits &= bits - 1;
+            const bool has1 = bits != 0ull;
+            const int j1 = has1 ? (int)__builtin_ctzll(bits) : j0;
+            bits &= bits - 1;
+            const int u0 = __builtin_amdgcn_readfirstlane(j0), u1 = __builtin_amdgcn_readfirstlane(j1);
+            const float4 co0 = st[u0], co1 = st[u1];
+            const float2 xy0 = *reinterpret_cast<const float2*>(st + NB + u0);
+            const float2 xy1 = *reinterpret_cast<const float2*>(st + NB + u1);
+            const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
+            const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
+            const f32x2 G = r3dg_expf2(pw0, pw1);
+            step(j0, true, pw0, G.x);
+            step(j1, has1, pw1, G.y);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        buf ^= 1;
+    }
+    // a block that stops early has no DMA in flight: every issued batch was waited for above
+    if (inside) {
+        const int pix = py * a.W + px;
+        a.out_depth[pix] = Dp;
+        a.out_stencil[pix] = St;
+    }
+}
+
+__global__ void __launch_bounds__(256) pack_inter_rec_kernel(int P, const int* __restrict__ radii,
+                                                             const float* __restrict__ depths,
+                                                             const float* __restrict__ stencils,
+                                                             const float* __restrict__ stencil_opacity,
+                                                             float4* __restrict__ inter_rec) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P || radii[i] <= 0) return;
+    inter_rec[i] = make_float4(depths[i], stencils[i], stencil_opacity[i], 0.f);
+}
+
+hipError_t launch_intermediate(const IntermediateArgs& a, int P, const int* radii, hipStream_t st) {
+    if (a.num_tiles == 0) return hipSuccess;
+    const char* e = getenv("R3DG_INTER");  // "reg": the register-staged kernel (A/B only)
+    if (e && e[0] == 'r') {
+        hipLaunchKernelGGL(intermediate_kernel, dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0, st, a);
+        return hipGetLastError();
+    }
+    if (P > 0)
+        hipLaunchKernelGGL(pack_inter_rec_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, radii, a.depths,
+                           a.stencils, a.stencil_opacity, a.inter_rec);
+    hipLaunchKernelGGL(intermediate_glds_kernel, dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+}
+
 // forward.cu:271-383 (RenderIntermediateTexturesCUDA): depth and stencil blend for the splat
 // shaders. Only launched when a non-default splat shader is active; the Stencil accumulator
 // starts at 0 (the reference leaves it uninitialised, forward.cu:312).
