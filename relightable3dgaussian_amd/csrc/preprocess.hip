@@ -545,11 +545,7 @@ hipError_t launch_bin_scatter(const BinArgs& a, hipStream_t st) {
 union TileDepthSortStorage {
     TileSortLds<4> s4;
     TileSortLds<R3DG_SORT_LONG_IPT> sl;
-    uint32_t bitonic[2 * kSortBT * R3DG_SORT_LONG_IPT];  // bitonic_sort_pairs' scratch
 };
-#ifndef R3DG_FWD_BITONIC
-#define R3DG_FWD_BITONIC 0  // 1: the chunks are sorted by the bitonic network (r3dg_tilesort.h)
-#endif
 
 __device__ __forceinline__ uint32_t nt_load(const uint32_t* p) { return __builtin_nontemporal_load(p); }
 
@@ -575,11 +571,7 @@ __device__ __forceinline__ void sort_tile_chunks(uint32_t s, uint32_t n, uint32_
             vals[k] = kv.y;
         }
         if (c > 0) __syncthreads();  // storage reuse
-#if R3DG_FWD_BITONIC
-        bitonic_sort_pairs<IPT>(keys, vals, (int)min(kChunk, n - c0), reinterpret_cast<uint32_t*>(&lds));
-#else
         sort_pairs_chunk<IPT>(keys, vals, (int)min(kChunk, n - c0), lds);
-#endif
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
             const uint32_t i = c0 + (uint32_t)(t * IPT + k);

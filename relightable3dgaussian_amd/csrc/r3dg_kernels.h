@@ -231,7 +231,6 @@ __device__ __forceinline__ uint32_t instance_slot(const uint32_t* offsets, float
     return (g == 0 ? 0u : offsets[g - 1]) + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
 }
 __global__ void xyz_normal_kernel(XyzNormalArgs a);
-__global__ void intermediate_kernel(IntermediateArgs a);
 // RenderIntermediateTextures: packs the per-Gaussian depth / stencil record, then the DMA-staged blend
 hipError_t launch_intermediate(const IntermediateArgs& a, int P, const int* radii, hipStream_t st);
 

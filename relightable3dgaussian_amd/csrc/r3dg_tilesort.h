@@ -64,84 +64,4 @@ __device__ __forceinline__ void sort_pairs_chunk(uint32_t (&keys)[IPT], uint32_t
     }
 }
 
-// (key, value) pairs compared lexicographically: the (depth bits, Gaussian id) order, total because
-// ids are distinct (pads, all-ones, compare equal among themselves and sort last)
-__device__ __forceinline__ bool pair_less(uint32_t ka, uint32_t va, uint32_t kb, uint32_t vb) {
-    return ka < kb || (ka == kb && va < vb);
-}
-
-// The same contract as sort_pairs_chunk (blocked arrangement in, blocked out, first n real) by a
-// bitonic network over N = the smallest power of two >= max(n, 64 * IPT) elements: element e =
-// thread * IPT + k. A stage of distance d compares e with e ^ d -- in registers for d < IPT, across
-// the wave's lanes by one shuffle per item for d < 64 * IPT, through LDS (one barrier pair) beyond;
-// e keeps the min when (e & d == 0) == (e & size == 0). No radix bookkeeping and no tie pass (the
-// pairs themselves are compared), and the waves of a small tile's network (n <= 64 * IPT) never meet
-// at a barrier. `lds`: 2 * kSortBT * IPT words of scratch, free on entry; a barrier ends the call.
-template <int IPT>
-__device__ __forceinline__ void bitonic_sort_pairs(uint32_t (&keys)[IPT], uint32_t (&vals)[IPT], int n,
-                                                   uint32_t* lds) {
-    static_assert((IPT & (IPT - 1)) == 0 && IPT <= 8, "power-of-two items per thread");
-    const int t = threadIdx.x;
-    int N = 64 * IPT;
-    while (N < n) N <<= 1;  // block-uniform, <= kSortBT * IPT
-    const bool act = t * IPT < N;  // whole waves
-    for (int size = 2; size <= N; size <<= 1) {
-        for (int d = size >> 1; d > 0; d >>= 1) {
-            if (d < IPT) {
-#pragma unroll
-                for (int dd = IPT / 2; dd >= 1; dd >>= 1) {
-                    if (dd != d) continue;
-#pragma unroll
-                    for (int k = 0; k < IPT; ++k) {
-                        if (k & dd) continue;
-                        const int kk = k | dd;
-                        const bool asc = ((t * IPT + k) & size) == 0;
-                        const uint32_t k0 = keys[k], v0 = vals[k], k1 = keys[kk], v1 = vals[kk];
-                        const bool sw = asc ? pair_less(k1, v1, k0, v0) : pair_less(k0, v0, k1, v1);
-                        keys[k] = sw ? k1 : k0;
-                        vals[k] = sw ? v1 : v0;
-                        keys[kk] = sw ? k0 : k1;
-                        vals[kk] = sw ? v0 : v1;
-                    }
-                }
-            } else if (d < 64 * IPT) {
-                const int ld = d / IPT;
-#pragma unroll
-                for (int k = 0; k < IPT; ++k) {
-                    const uint32_t pk = (uint32_t)__shfl_xor((int)keys[k], ld);
-                    const uint32_t pv = (uint32_t)__shfl_xor((int)vals[k], ld);
-                    const int e = t * IPT + k;
-                    const bool lowmin = ((e & d) == 0) == ((e & size) == 0);
-                    const bool take = lowmin ? pair_less(pk, pv, keys[k], vals[k]) : pair_less(keys[k], vals[k], pk, pv);
-                    keys[k] = take ? pk : keys[k];
-                    vals[k] = take ? pv : vals[k];
-                }
-            } else {
-                __syncthreads();  // earlier readers of lds are done
-                if (act) {
-#pragma unroll
-                    for (int k = 0; k < IPT; ++k) {
-                        lds[t * IPT + k] = keys[k];
-                        lds[kSortBT * IPT + t * IPT + k] = vals[k];
-                    }
-                }
-                __syncthreads();
-                if (act) {
-#pragma unroll
-                    for (int k = 0; k < IPT; ++k) {
-                        const int e = t * IPT + k, p = e ^ d;
-                        const uint32_t pk = lds[p], pv = lds[kSortBT * IPT + p];
-                        const bool lowmin = ((e & d) == 0) == ((e & size) == 0);
-                        const bool take =
-                            lowmin ? pair_less(pk, pv, keys[k], vals[k]) : pair_less(keys[k], vals[k], pk, pv);
-                        keys[k] = take ? pk : keys[k];
-                        vals[k] = take ? pv : vals[k];
-                    }
-                }
-            }
-        }
-    }
-    __syncthreads();
-}
-
 }  // namespace r3dg

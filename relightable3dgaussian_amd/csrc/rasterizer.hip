@@ -802,11 +802,15 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     // forward's duplicate pass (a row's presence depends on the forward state only)
     // the backward blend addresses partial rows with 32-bit offsets in float4 units
     R3DG_REQUIRE((size_t)RS * (size_t)L < (1ull << 32), "rasterize_gaussians_backward: too many tile instances");
-    // R3DG_BWD_REDUCE=atomic: the backward blend adds its (instance, wave) rows into the per-Gaussian
-    // sums with f32 atomics (no partial rows, flags or row_sum_kernel; order-dependent last bits)
+    // The second stage of the per-instance reduction (backward.cu:552-611 accumulates per pixel with
+    // atomics). Default: the backward blend adds each (instance, wave) row into the per-Gaussian sums
+    // with f32 atomics (no partial rows, flags or row_sum_kernel; last bits depend on arrival order,
+    // as the reference's do; M1: step 2.00 -> 1.94 ms). R3DG_BWD_REDUCE=rows: partial rows summed in
+    // a fixed order by row_sum_kernel, bitwise reproducible run to run.
     const bool atomic_sums = [] {
         const char* e = getenv("R3DG_BWD_REDUCE");  // read per call: tests switch it at run time
-        return e && e[0] == 'a';
+        const char* v = getenv("R3DG_BWD");          // the DPP cross-check kernel writes partial rows
+        return !(e && e[0] == 'r') && !(v && v[0] == 'd');
     }();
     // atomic sums: [X part | 6 moments | pad] per Gaussian, rows of 32 floats (128 B) so each
     // 16-float X segment is one aligned 64-B atomic request

@@ -300,23 +300,29 @@ __device__ __forceinline__ void split_bf16x3(const float (&x)[8], bf16x8& h, bf1
 }
 
 #ifndef R3DG_BWD_SPLIT
-#define R3DG_BWD_SPLIT 3  // bf16 terms per f32 value in the flush's MFMA products: 3 = exact f32
-                          // products; 2 = two-term splits (relative error < 2^-15 per product)
+#define R3DG_BWD_SPLIT 2  // bf16 terms per f32 value of w and q in the flush's MFMA products: 2 =
+                          // h + m, |x - h - m| <= 2^-16 |x| unbiased (measured M1: render_bwd
+                          // 0.765 -> 0.711 ms); 3 = exact f32 products
 #endif
 
-// x = h + m to within 2^-15 |x| (two-term form of split_bf16x3)
+// x = h + m to within 2^-16 |x|: h the truncated top 8 significant bits (v_and + v_perm per pair),
+// m = x - h (exact) rounded to nearest bf16 (one v_cvt_pk_bf16_f32 per pair), so the residual is
+// unbiased (a truncated m would shrink every |w| and |q| by up to 2^-14)
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split_bf16x2(const float (&x)[8], bf16x8& h, bf16x8& m) {
-    uint32_t ux[8], ur[8];
+    uint32_t ux[8];
+    float r[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         ux[i] = __float_as_uint(x[i]);
-        ur[i] = __float_as_uint(x[i] - __uint_as_float(ux[i] & 0xffff0000u));
+        r[i] = x[i] - __uint_as_float(ux[i] & 0xffff0000u);
     }
     bf16x8_u H, M;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         H.u[k] = hi16_pair(ux[2 * k], ux[2 * k + 1]);
-        M.u[k] = hi16_pair(ur[2 * k], ur[2 * k + 1]);
+        M.u[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v{r[2 * k], r[2 * k + 1]}), bf16x2v));
     }
     h = H.v;
     m = M.v;

@@ -14,7 +14,7 @@
 //     per sorted position (bit = quadrant), the exact visit list of the backward (render_bwd.hip);
 //   * early exit per wave (ballot) and per block (__syncthreads_count), as the reference;
 //   * XCD-aware tile order (r3dg_kernels.h).
-// render_fwd_shader_kernel blends the splat-shader colour as well (non-default splat shaders).
+// render_fwd_glds_kernel<SMAX, true> blends the splat-shader colour as well (non-default splat shaders).
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
 #include "r3dg_tilesort.h"
@@ -30,193 +30,13 @@ R3DG_EXP_READER(r3dg_exp_counters_fwd)
 #endif
 
 // ---------------------------------------------------------------------------------------------
-// Splat-shader blend (a non-default splat shader is active): the per-Gaussian shader colour is not
-// part of the render record, so instances are staged from the SoA geometry state by registers,
-// 256 per batch, two block barriers per batch. Blends colour and shader colour with the same step
-// as render_fwd_glds_kernel and writes the same contribution bits.
-// ---------------------------------------------------------------------------------------------
-template <int SMAX>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? 4 : 1)))
-render_fwd_shader_kernel(RenderFwdArgs a) {
-    constexpr int NB = kBlock;                         // instances staged per batch
-    constexpr int FO = 8;                              // feature offset inside the attribute row
-    constexpr int NA4 = (FO + SMAX + 3) / 4;           // float4 per attribute row
-    __shared__ float2 s_xy[NB];
-    __shared__ float4 s_co[NB];
-    __shared__ float4 s_attr[NA4 * NB];                // q-major: float4 q of instance j at q*NB + j
-                                                       // (staging writes 16-B strided: conflict-free)
-    __shared__ uint32_t s_bits[NB / 32][4];            // [32-instance chunk][wave]: live-instance masks
-    __shared__ uint32_t s_cw[NB / 32][4];              // [chunk][wave]: contribution bits of the batch
-
-    const int tile = block_tile(a.tile_order, a.num_tiles);
-    if (tile >= a.num_tiles) return;
-    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
-    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
-    const bool inside = px < a.W && py < a.H;
-    const float pfx = (float)px, pfy = (float)py;
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
-    bool done = !inside;
-    float T = 1.0f;
-    uint32_t last = 0;
-    float C[3] = {0.f, 0.f, 0.f}, CS[3] = {0.f, 0.f, 0.f}, F[SMAX > 0 ? SMAX : 1];
-    float Dp = 0.f, Op = 0.f;
-#pragma unroll
-    for (int c = 0; c < SMAX; ++c) F[c] = 0.f;
-
-    // contribution byte of instance t of the batch at b0 (render_fwd_glds_kernel's layout)
-    auto write_bits = [&](int b0, int cnt) {
-        if (t < cnt) {
-            const int c = t >> 5, sh = t & 31;
-            const uint32_t v = ((s_cw[c][0] >> sh) & 1u) | ((s_cw[c][1] >> sh) & 1u) << 1 |
-                               ((s_cw[c][2] >> sh) & 1u) << 2 | ((s_cw[c][3] >> sh) & 1u) << 3;
-            a.contrib[range.x + (uint32_t)(b0 + t)] = (uint8_t)v;
-        }
-    };
-    // Gaussian ids loaded one batch ahead: staging waits for one dependent round trip, not two
-    uint32_t gid_next = t < n ? a.point_list[range.x + t] : 0u;
-    int base = 0;
-    for (; base < n; base += NB) {
-        const bool all_done = __syncthreads_count(done) == kBlock;
-        if (base > 0) write_bits(base - NB, NB);  // s_cw is rewritten only after the next barrier
-        if (all_done) break;
-        uint32_t m = 0;
-        if (base + t < n) {
-            const uint32_t gid = gid_next;
-            gid_next = (base + NB + t < n) ? a.point_list[range.x + base + NB + t] : 0u;
-            const float2 xy = a.means2D[gid];
-            const float4 co = a.conic_opacity[gid];
-            s_xy[t] = xy;
-            s_co[t] = co;
-            m = quadrant_mask(xy, co, tx * kTileX, ty * kTileY, a.cull);
-            float v[NA4 * 4];
-#pragma unroll
-            for (int i = 0; i < NA4 * 4; ++i) v[i] = 0.f;
-            v[0] = a.colors[3 * gid + 0];
-            v[1] = a.colors[3 * gid + 1];
-            v[2] = a.colors[3 * gid + 2];
-            v[3] = a.depths[gid];
-            v[4] = a.shader_colors[3 * gid + 0];
-            v[5] = a.shader_colors[3 * gid + 1];
-            v[6] = a.shader_colors[3 * gid + 2];
-            const float* f = a.features + (size_t)gid * a.S;
-#pragma unroll
-            for (int c = 0; c < SMAX; ++c)
-                if (c < a.S) v[FO + c] = f[c];
-#pragma unroll
-            for (int q = 0; q < NA4; ++q)
-                s_attr[q * NB + t] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-        }
-        // compaction: this wave's 64 staged slots are chunks 2w and 2w+1; one ballot per target wave
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const unsigned long long bal = __ballot((m >> b) & 1u);
-            if (l == 0) {
-                s_bits[2 * w][b] = (uint32_t)bal;
-                s_bits[2 * w + 1][b] = (uint32_t)(bal >> 32);
-            }
-        }
-        __syncthreads();
-        // One blend step of renderCUDA (forward.cu:470-520): the tests are predicated, every LDS
-        // read of the instance is issued before them, and only the accumulation is a branch.
-        // `power` and G = r3dg_expf(power) come from the caller (a pair's two exps run packed).
-        uint32_t cw = 0u;  // contribution bits of the current chunk
-        auto step = [&](int j, bool live, float opacity, float power, float G) {
-#pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
-            float v[NA4 * 4];
-#pragma unroll
-            for (int q = 0; q < NA4; ++q) {
-                const float4 r = s_attr[q * NB + j];
-                v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
-            }
-            const float alpha = fminf(0.99f, opacity * G);  // bit-identical to the oracle
-            const bool contrib = live && !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-            const float test_T = T * (1.0f - alpha);
-            const bool stop = test_T < 0.0001f;
-            done = done || (contrib && stop);
-            if (__ballot(contrib && !stop) != 0ull) cw |= 1u << (__builtin_amdgcn_readfirstlane(j) & 31);
-            if (contrib && !stop) {
-                const float wgt = alpha * T;
-                C[0] = __builtin_fmaf(v[0], wgt, C[0]);
-                C[1] = __builtin_fmaf(v[1], wgt, C[1]);
-                C[2] = __builtin_fmaf(v[2], wgt, C[2]);
-                CS[0] = __builtin_fmaf(v[4], wgt, CS[0]);
-                CS[1] = __builtin_fmaf(v[5], wgt, CS[1]);
-                CS[2] = __builtin_fmaf(v[6], wgt, CS[2]);
-#pragma unroll
-                for (int c2 = 0; c2 < SMAX; ++c2) F[c2] = __builtin_fmaf(v[FO + c2], wgt, F[c2]);
-                Dp = __builtin_fmaf(v[3], wgt, Dp);
-                Op += wgt;
-                T = test_T;
-                last = (uint32_t)(base + j + 1);
-            }
-        };
-        bool alive = __ballot(!done) != 0ull;
-        for (int c = 0; c < NB / 32; ++c) {
-            uint32_t bits = alive ? __builtin_amdgcn_readfirstlane(s_bits[c][w]) : 0u;
-            cw = 0u;
-            while (bits) {
-                // two compacted instances per iteration (the second one's reads overlap the first)
-                const int j0 = c * 32 + __builtin_ctz(bits);
-                bits &= bits - 1;
-                const bool has1 = bits != 0u;
-                const int j1 = has1 ? c * 32 + __builtin_ctz(bits) : j0;
-                bits &= bits - 1;
-                const float4 co0 = s_co[j0], co1 = s_co[j1];
-                const float2 xy0 = s_xy[j0], xy1 = s_xy[j1];
-                const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
-                const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
-                const f32x2 G = r3dg_expf2(pw0, pw1);  // both exps at once: neither depends on T
-                step(j0, true, co0.w, pw0, G.x);
-                step(j1, has1, co1.w, pw1, G.y);
-                if (__ballot(!done) == 0ull) {  // converged here: a uniform exit
-                    alive = false;
-                    break;
-                }
-            }
-            if (l == 0) s_cw[c][w] = cw;
-        }
-    }
-    if (base >= n && n > 0) {  // ran to the end: the last batch's bits (block-uniform)
-        __syncthreads();
-        const int b0 = (n - 1) / NB * NB;
-        write_bits(b0, n - b0);
-    }
-
-    if (inside) {
-        const int pix = py * a.W + px;
-        a.final_T[pix] = T;
-        a.n_contrib[pix] = last;
-        const float b0 = a.bg[0], b1 = a.bg[1], b2 = a.bg[2];
-        a.out_color[3 * pix + 0] = C[0] + T * b0;
-        a.out_color[3 * pix + 1] = C[1] + T * b1;
-        a.out_color[3 * pix + 2] = C[2] + T * b2;
-        a.out_shader_color[3 * pix + 0] = CS[0] + T * b0;
-        a.out_shader_color[3 * pix + 1] = CS[1] + T * b1;
-        a.out_shader_color[3 * pix + 2] = CS[2] + T * b2;
-        a.out_depth[pix] = Dp;
-        a.out_opacity[pix] = Op;
-        if (a.zero_stencil) a.zero_stencil[pix] = 0.f;
-#pragma unroll
-        for (int c = 0; c < SMAX; ++c)
-            if (c < a.S) a.out_feature[a.flay.a[c] + pix * a.flay.m[c]] = F[c];
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
 // The default-shader blend (render records only): the records of batch b+1 are copied HBM -> LDS
 // by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no staging stores) while the waves blend batch b,
 // so the record round trip leaves the critical path and a batch costs one block barrier (the
 // early-exit count). Every wave evaluates the exact quadrant cull of the staged instances for its
 // own quadrant. Staging layout: column q (float4 q of the render record) of instance j at
-// [q * NB + j]. Same blend step, same decisions and sums as render_fwd_shader_kernel (bitwise).
+// [q * NB + j].
 // ---------------------------------------------------------------------------------------------
-#ifndef R3DG_FWD_BITONIC
-#define R3DG_FWD_BITONIC 0  // fused sort: 1 = bitonic network (r3dg_tilesort.h), 0 = rocPRIM radix passes
-#endif
-
 #ifndef R3DG_FWDG_NB
 #define R3DG_FWDG_NB 64  // instances per staged batch (two resident: 12.3 KB, 64 VGPRs -> 8 waves/SIMD;
                          // 128: 24.6 KB -> 6 waves/SIMD, measured 0.480 vs 0.447 ms at M1)
@@ -241,9 +61,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     static_assert(NB == 64, "one 64-bit contribution word per wave and batch");
     // one LDS array: [2 staging buffers | 2 x 64 x 4 contribution flags (batch buffer, instance, wave)
     // | the tile's sorted Gaussian ids (fused sort)]; the fused sort's scratch aliases the staging
-    constexpr int SORT4a = (int)((sizeof(TileSortLds<kFusedSortMax / kSortBT>) + 15) / 16);
-    constexpr int SORT4b = 2 * kFusedSortMax / 4;              // bitonic_sort_pairs' key / value scratch
-    constexpr int SORT4 = SORT4a > SORT4b ? SORT4a : SORT4b;
+    constexpr int SORT4 = (int)((sizeof(TileSortLds<kFusedSortMax / kSortBT>) + 15) / 16);
     constexpr int STG = 2 * SBUF > SORT4 ? 2 * SBUF : SORT4;  // float4 of staging / sort scratch
     __shared__ float4 s_lds[STG + 32 + kFusedSortMax / 4];
     uint8_t* const s_cf = reinterpret_cast<uint8_t*>(s_lds + STG);
@@ -277,11 +95,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
             vals[k] = kv.y;
         }
 #ifndef R3DG_EXP_NOSORT  // timing experiment only (results invalid): the blend without the fused sort
-#if R3DG_FWD_BITONIC
-        if (n > 1) bitonic_sort_pairs<IPT>(keys, vals, n, reinterpret_cast<uint32_t*>(s_lds));
-#else
         if (n > 1) sort_pairs_chunk<IPT>(keys, vals, n, *reinterpret_cast<TileSortLds<IPT>*>(s_lds));
-#endif
 #endif
 #pragma unroll
         for (int k = 0; k < IPT; ++k) {
@@ -493,10 +307,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
 template <int SMAX>
 static hipError_t launch_fwd_s(const RenderFwdArgs& a, bool shader, hipStream_t stream) {
     const int grid = padded_tile_grid(a.num_tiles);
-    const char* e = getenv("R3DG_FWD_SHADER");  // "reg": the register-staged shader kernel (A/B only)
-    if (shader && e && e[0] == 'r')
-        launch_kernel(render_fwd_shader_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
-    else if (shader)
+    if (shader)
         launch_kernel(render_fwd_glds_kernel<SMAX, true>, dim3(grid), dim3(kBlock), stream, a);
     else
         launch_kernel(render_fwd_glds_kernel<SMAX, false>, dim3(grid), dim3(kBlock), stream, a);
@@ -522,8 +333,9 @@ hipError_t launch_render_forward(const RenderFwdArgs& a, bool shader, hipStream_
 // opacities (an instance it skips fails both alpha tests on every pixel of the quadrant) and
 // steps through the survivors two at a time (both exps packed). The arithmetic is the oracle's
 // (oracle_render_intermediate: contraction off, plain products), the Stencil accumulator starts
-// at 0 (the reference leaves it uninitialised, forward.cu:312). Replaces the register-staged
-// 256-instance kernel below, which evaluated every (instance, pixel) pair of the tile list.
+// at 0 (the reference leaves it uninitialised, forward.cu:312). The register-staged 256-instance
+// kernel it replaced evaluated every (instance, pixel) pair of the tile list: 0.97 ms per pass at
+// M1.
 __global__ void __launch_bounds__(kBlock) intermediate_glds_kernel(IntermediateArgs a) {
 #pragma clang fp contract(off)
     constexpr int NB = 64, NCOL = 3, SBUF = NCOL * NB;
@@ -633,74 +445,11 @@ __global__ void __launch_bounds__(256) pack_inter_rec_kernel(int P, const int* _
 
 hipError_t launch_intermediate(const IntermediateArgs& a, int P, const int* radii, hipStream_t st) {
     if (a.num_tiles == 0) return hipSuccess;
-    const char* e = getenv("R3DG_INTER");  // "reg": the register-staged kernel (A/B only)
-    if (e && e[0] == 'r') {
-        hipLaunchKernelGGL(intermediate_kernel, dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0, st, a);
-        return hipGetLastError();
-    }
     if (P > 0)
         hipLaunchKernelGGL(pack_inter_rec_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, radii, a.depths,
                            a.stencils, a.stencil_opacity, a.inter_rec);
     hipLaunchKernelGGL(intermediate_glds_kernel, dim3(padded_tile_grid(a.num_tiles)), dim3(kBlock), 0, st, a);
     return hipGetLastError();
-}
-
-// forward.cu:271-383 (RenderIntermediateTexturesCUDA): depth and stencil blend for the splat
-// shaders. Only launched when a non-default splat shader is active; the Stencil accumulator
-// starts at 0 (the reference leaves it uninitialised, forward.cu:312).
-__global__ void __launch_bounds__(kBlock) intermediate_kernel(IntermediateArgs a) {
-    __shared__ float2 s_xy[kBlock];
-    __shared__ float4 s_co[kBlock];
-    __shared__ float2 s_ds[kBlock];  // depth, stencil value
-    __shared__ float s_so[kBlock];
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
-    if (tile >= a.num_tiles) return;
-    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int px = tx * kTileX + (w & 1) * 8 + (l & 7);
-    const int py = ty * kTileY + (w >> 1) * 8 + (l >> 3);
-    const bool inside = px < a.W && py < a.H;
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
-    bool done = !inside;
-    float sT = 1.f, T = 1.f, St = 0.f, Dp = 0.f;
-    for (int base = 0; base < n; base += kBlock) {
-        if (__syncthreads_count(done) == kBlock) break;
-        if (base + t < n) {
-            const uint32_t gid = a.point_list[range.x + base + t];
-            s_xy[t] = a.means2D[gid];
-            s_co[t] = a.conic_opacity[gid];
-            s_ds[t] = make_float2(a.depths[gid], a.stencils[gid]);
-            s_so[t] = a.stencil_opacity[gid];
-        }
-        __syncthreads();
-        const int cnt = min(kBlock, n - base);
-        for (int j = 0; !done && j < cnt; ++j) {
-            const float2 xy = s_xy[j];
-            const float4 co = s_co[j];
-            const float dx = xy.x - (float)px, dy = xy.y - (float)py;
-            const float power = gauss_power(co, dx, dy);
-            if (power > 0.0f) continue;
-            const float G = r3dg_expf(power);
-            const float alpha = fminf(0.99f, co.w * G);
-            const float salpha = fminf(0.99f, s_so[j] * G);
-            if (alpha < 1.0f / 255.0f && salpha < 1.0f / 255.0f) continue;
-            const float tT = T * (1 - alpha), tS = sT * (1 - salpha);
-            if (tT < 0.0001f && tS < 0.0001f) {
-                done = true;
-                continue;
-            }
-            Dp += s_ds[j].x * (alpha * T);
-            T = tT;
-            St += s_ds[j].y * (salpha * sT);
-            sT = tS;
-        }
-    }
-    if (inside) {
-        const int pix = py * a.W + px;
-        a.out_depth[pix] = Dp;
-        a.out_stencil[pix] = St;
-    }
 }
 
 // forward.cu:564-658 (renderSurfaceXYZCUDA + renderPseudoNormalCUDA) fused: every thread

@@ -101,3 +101,28 @@ def assert_brdf(name, got, ref, summed=False):
         assert_close(name, got, ref, 1e-4 * max(float(np.abs(ref).max()), 1e-12), 1e-4)
     else:
         assert_close(name, got, ref, 1e-4, 0.0)
+
+
+import contextlib  # noqa: E402
+
+
+class rows_reduction(contextlib.ContextDecorator):
+    """Context manager / decorator: the backward's deterministic reduction (R3DG_BWD_REDUCE=rows: partial rows
+    summed in a fixed order) for tests that compare two HIP backward runs bit for bit; the default
+    atomic flush is order-dependent in the last bits, as the reference's atomics are."""
+
+    def __enter__(self):
+        import os
+
+        self.prev = os.environ.get("R3DG_BWD_REDUCE")
+        os.environ["R3DG_BWD_REDUCE"] = "rows"
+        return self
+
+    def __exit__(self, *exc):
+        import os
+
+        if self.prev is None:
+            os.environ.pop("R3DG_BWD_REDUCE", None)
+        else:
+            os.environ["R3DG_BWD_REDUCE"] = self.prev
+        return False

@@ -14,7 +14,7 @@ import pytest
 
 import oracle
 from relightable3dgaussian_amd import synthetic
-from tests._helpers import assert_brdf, assert_close, hip_backward, hip_forward, tt, upstream_grads
+from tests._helpers import assert_brdf, assert_close, rows_reduction, hip_backward, hip_forward, tt, upstream_grads
 
 pytestmark = pytest.mark.gpu
 
@@ -118,6 +118,7 @@ def test_dense_tiles_depth_sort(hip_ext):
         assert_close(k, gh[k], go[k], _grad_tol(go[k]), 2e-3)
 
 
+@rows_reduction()
 def test_cull_is_exact(hip_ext):
     """The per-quadrant footprint skip must not change a single bit (render_fwd.hip)."""
     scene, cam = synthetic.small_scene(P=5000, S=11, seed=3, width=128, height=96, scale_range=(0.005, 0.3))
@@ -139,13 +140,14 @@ def test_cull_is_exact(hip_ext):
 def _cull_on_off(hip_ext, scene, cam, S=11, seed=1):
     a = hip_forward(hip_ext, scene, cam, S=S)
     dc, do, dd, df = upstream_grads(cam.height, cam.width, S, seed=seed)
-    ga = hip_backward(hip_ext, a, dc, do, dd, df)
-    os.environ["R3DG_NO_CULL"] = "1"
-    try:
-        b = hip_forward(hip_ext, scene, cam, S=S)
-        gb = hip_backward(hip_ext, b, dc, do, dd, df)
-    finally:
-        del os.environ["R3DG_NO_CULL"]
+    with rows_reduction():  # the two backward runs are compared bit for bit
+        ga = hip_backward(hip_ext, a, dc, do, dd, df)
+        os.environ["R3DG_NO_CULL"] = "1"
+        try:
+            b = hip_forward(hip_ext, scene, cam, S=S)
+            gb = hip_backward(hip_ext, b, dc, do, dd, df)
+        finally:
+            del os.environ["R3DG_NO_CULL"]
     for k in ["color", "opacity", "depth", "feature", "n_contrib", "normal", "surface_xyz"]:
         np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
     for k in ga:
@@ -278,22 +280,16 @@ def test_backward_deterministic(hip_ext):
     """The deterministic reduction (R3DG_BWD_REDUCE=rows: partial rows summed in a fixed order) gives
     bitwise the same gradients run to run."""
     scene, cam = synthetic.small_scene(P=3000, S=11, seed=2, width=96, height=96)
-    prev = os.environ.get("R3DG_BWD_REDUCE")
-    os.environ["R3DG_BWD_REDUCE"] = "rows"
-    try:
+    with rows_reduction():
         h = hip_forward(hip_ext, scene, cam, S=11)
         dc, do, dd, df = upstream_grads(cam.height, cam.width, 11)
         g1 = hip_backward(hip_ext, h, dc, do, dd, df)
         g2 = hip_backward(hip_ext, h, dc, do, dd, df)
-    finally:
-        if prev is None:
-            del os.environ["R3DG_BWD_REDUCE"]
-        else:
-            os.environ["R3DG_BWD_REDUCE"] = prev
     for k in g1:
         np.testing.assert_array_equal(g1[k], g2[k], err_msg=k)
 
 
+@rows_reduction()
 def test_backward_ex_layouts(hip_ext):
     """HWC colour / native feature grads (the wrapper's entry) == CHW / planar (reference contract)."""
     import torch
@@ -440,6 +436,7 @@ def test_binning_large_frames(hip_ext, size):
     assert _keys_vs_oracle(hip_ext, scene, cam, h) > 100_000
 
 
+@rows_reduction()
 def test_binning_atomic_path_matches(hip_ext):
     """The global-atomic binning (R3DG_BIN=atomic, the fallback above kBinMaxTiles) and the LDS
     binning give bit-identical sorted lists, images and gradients; both match the oracle's keys."""
@@ -661,6 +658,7 @@ def test_backward_mfma_matches_dpp_variant(hip_ext, S):
                      1e-3)
 
 
+@rows_reduction()
 def test_backward_chunked_delivery(hip_ext):
     """Chunked per-Gaussian phase (r3dg_backward_outputs.n_chunks / chunk_done): bitwise the same
     gradients as one chunk; the callback sees 256-aligned ranges covering every Gaussian in order,
@@ -694,6 +692,7 @@ def _chunked_exchange_worker(rank, world, port, q, mode="views"):
     import torch
     import torch.distributed as dist
 
+    os.environ["R3DG_BWD_REDUCE"] = "rows"  # local and exchanged backward runs are compared bitwise
     import relightable3dgaussian_amd as r3
     from relightable3dgaussian_amd import view_parallel
 
