@@ -300,9 +300,15 @@ __device__ __forceinline__ void split_bf16x3(const float (&x)[8], bf16x8& h, bf1
 }
 
 #ifndef R3DG_BWD_SPLIT
-#define R3DG_BWD_SPLIT 2  // bf16 terms per f32 value of w and q in the flush's MFMA products: 2 =
-                          // h + m, |x - h - m| <= 2^-16 |x| unbiased (measured M1: render_bwd
-                          // 0.765 -> 0.711 ms); 3 = exact f32 products
+#define R3DG_BWD_SPLIT 2  // bf16 terms per f32 value of w (= alpha T: colour / feature / depth grads)
+                          // in the flush's MFMA products: 2 = h + m, |x - h - m| <= 2^-16 |x|
+                          // unbiased; 3 = exact f32 products
+#endif
+#ifndef R3DG_BWD_SPLIT_Q
+#define R3DG_BWD_SPLIT_Q 3  // the same for q = G dL/dalpha (the moments behind the mean2D / conic /
+                            // opacity grads): exact, as the conic inverse amplifies their errors by up
+                            // to ~1e6 on needle-shaped splats (test_cull_exact_needles: with 2 terms
+                            // one needle's dL/dmeans3D left the fp32 sensitivity bound 88x)
 #endif
 
 // x = h + m to within 2^-16 |x|: h the truncated top 8 significant bits (v_and + v_perm per pair),
@@ -534,7 +540,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) qv[i] = src[i];
             bf16x8 h, m, o;
-#if R3DG_BWD_SPLIT == 2
+#if R3DG_BWD_SPLIT_Q == 2
             split_bf16x2(qv, h, m);
             (void)o;
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, yb[b], accY, 0, 0, 0);
