@@ -207,6 +207,7 @@ def test_cull_exact_needles(hip_ext):
         assert np.all(diff <= bound), (k, int((diff > bound).sum()), float((diff / bound).max()))
 
 
+@rows_reduction()  # the feature gradients of two backward runs are compared bit for bit
 def test_backward_geometry_false(hip_ext):
     """backward_geometry=False drops the feature term of dL/dalpha (backward.cu:563): matches the
     oracle run the same way, and differs from the default where features carry gradient."""
