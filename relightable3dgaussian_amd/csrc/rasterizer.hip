@@ -229,22 +229,37 @@ __global__ void __launch_bounds__(256) init_stencil_kernel(int P, float* stencil
 
 // Splat shaders edit conic_opacity.w after the render records were written: refresh the records'
 // opacity (the backward reads records; the reference's backward reads the edited geometry state).
-// Also writes the shader record of every visible Gaussian (render_fwd_glds_kernel<SMAX, true>):
-// rec4 - 2 float4 in the attribute row's layout, [shader colour, 0 | the splat shaders' features,
-// zero padded] -- the blend's staged colour and feature columns after the splat shaders ran.
 __global__ void __launch_bounds__(256) refresh_record_opacity_kernel(int P, const int* __restrict__ radii,
                                                                      const float4* __restrict__ conic_opacity,
-                                                                     float4* __restrict__ records, int rec4,
-                                                                     const float* __restrict__ shader_rgb,
-                                                                     const float* __restrict__ feats, int S,
-                                                                     float* __restrict__ shader_rec) {
+                                                                     float4* __restrict__ records, int rec4) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P || radii[i] <= 0) return;
     records[(size_t)i * rec4].w = conic_opacity[i].w;
-    const int nf = 4 * (rec4 - 2);
-    float* o = shader_rec + (size_t)i * nf;
-    o[0] = shader_rgb[3 * i]; o[1] = shader_rgb[3 * i + 1]; o[2] = shader_rgb[3 * i + 2]; o[3] = 0.f;
-    for (int c = 4; c < nf; ++c) o[c] = c - 4 < S ? feats[(size_t)i * S + (c - 4)] : 0.f;
+}
+
+// The shader record of every visible Gaussian (render_fwd_glds_kernel<SMAX, true>): na4 float4 in
+// the attribute row's layout, [shader colour, 0 | the splat shaders' features, zero padded] -- the
+// blend's staged colour and feature columns after the splat shaders ran. One thread per float4, so
+// the stores are coalesced (a thread per Gaussian wrote a 112-byte row each: 0.37 ms at 1 M, S = 21).
+__global__ void __launch_bounds__(256) shader_record_kernel(int P, int na4, const int* __restrict__ radii,
+                                                            const float* __restrict__ shader_rgb,
+                                                            const float* __restrict__ feats, int S,
+                                                            float4* __restrict__ shader_rec) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (long long)P * na4) return;
+    const int i = (int)(e / na4), q = (int)(e - (long long)i * na4);
+    if (radii[i] <= 0) return;
+    float v[4];
+    if (q == 0) {
+        v[0] = shader_rgb[3 * i]; v[1] = shader_rgb[3 * i + 1]; v[2] = shader_rgb[3 * i + 2]; v[3] = 0.f;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = 4 * (q - 1) + k;
+            v[k] = c < S ? feats[(size_t)i * S + c] : 0.f;
+        }
+    }
+    shader_rec[e] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
 // ---- shader registry (ShShader.cu:196-230, splatShader.cu:283-333, postProcessShader.cu:395-436) ----
@@ -688,8 +703,10 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
             R3DG_CHECK_LAUNCH(s->debug, st);
         }
         hipLaunchKernelGGL(refresh_record_opacity_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P, radii,
-                           geom.conic_opacity, geom.records, record_f4(S), geom.shader_rgb, feats, S,
-                           reinterpret_cast<float*>(shader_rec));
+                           geom.conic_opacity, geom.records, record_f4(S));
+        const int na4 = record_f4(S) - 2;
+        hipLaunchKernelGGL(shader_record_kernel, dim3((unsigned)(((long long)P * na4 + 255) / 256)), dim3(256), 0, st,
+                           P, na4, radii, geom.shader_rgb, feats, S, shader_rec);
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 

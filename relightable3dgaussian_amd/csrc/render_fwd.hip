@@ -390,21 +390,23 @@ __global__ void __launch_bounds__(kBlock) intermediate_glds_kernel(IntermediateA
             mine = quadrant_live(make_float2(r1.x, r1.y), co, qx0, qy0, 1);
         }
         unsigned long long bits = __ballot(mine);
+        // the tests predicated, only the accumulation a branch (as the blend's step)
         auto step = [&](int j, bool live, float power, float G) {
             const int ju = __builtin_amdgcn_readfirstlane(j);
             const float o = st[ju].w;
             const float4 ds = st[2 * NB + ju];  // depth, stencil, stencil opacity
             const float alpha = fminf(0.99f, o * G), salpha = fminf(0.99f, ds.z * G);
-            if (!live || done || power > 0.0f || (alpha < 1.0f / 255.0f && salpha < 1.0f / 255.0f)) return;
+            const bool contrib = live && !done && !(power > 0.0f) &&
+                                 !(alpha < 1.0f / 255.0f && salpha < 1.0f / 255.0f);
             const float tT = T * (1 - alpha), tS = sT * (1 - salpha);
-            if (tT < 0.0001f && tS < 0.0001f) {
-                done = true;
-                return;
+            const bool stop = tT < 0.0001f && tS < 0.0001f;
+            done = done || (contrib && stop);
+            if (contrib && !stop) {
+                Dp += ds.x * (alpha * T);
+                T = tT;
+                St += ds.y * (salpha * sT);
+                sT = tS;
             }
-            Dp += ds.x * (alpha * T);
-            T = tT;
-            St += ds.y * (salpha * sT);
-            sT = tS;
         };
         while (bits && __ballot(!done) != 0ull) {
             const int j0 = (int)__builtin_ctzll(bits);
