@@ -971,17 +971,19 @@ static void brdf_eval(int idx, int S_inc, int S_dir, int S_vis, const float* bas
                       const float* d, const float* coef, brdf_sample* s)
 {
     for (int c = 0; c < 3; ++c) s->local[c] = 0.f;
+    /* the SH light sums as fmaf chains in coefficient order (brdf.hip eval_lights; nvcc contracts the
+     * reference's `+= a * b` the same way) */
     for (int i = 0; i < S_inc; ++i)
-        for (int c = 0; c < 3; ++c) s->local[c] += inc[((size_t)idx * S_inc + i) * 3 + c] * coef[i];
+        for (int c = 0; c < 3; ++c) s->local[c] = fmaf(inc[((size_t)idx * S_inc + i) * 3 + c], coef[i], s->local[c]);
     for (int c = 0; c < 3; ++c) s->local[c] = fmaxf(s->local[c], 0.0f);
     for (int c = 0; c < 3; ++c) s->global[c] = 0.5f;
     for (int i = 0; i < S_dir; ++i)
-        for (int c = 0; c < 3; ++c) s->global[c] += dir_shs[i * 3 + c] * coef[i];
+        for (int c = 0; c < 3; ++c) s->global[c] = fmaf(dir_shs[i * 3 + c], coef[i], s->global[c]);
     for (int c = 0; c < 3; ++c) s->global[c] = fmaxf(s->global[c], 0.0f);
     float vis = 0.5f;
-    for (int i = 0; i < S_vis; ++i) vis += vis_shs[(size_t)idx * S_vis + i] * coef[i];
+    for (int i = 0; i < S_vis; ++i) vis = fmaf(vis_shs[(size_t)idx * S_vis + i], coef[i], vis);
     s->vis = fmaxf(0.0f, fminf(vis, 1.0f));
-    for (int c = 0; c < 3; ++c) s->light[c] = s->vis * s->global[c] + s->local[c];
+    for (int c = 0; c < 3; ++c) s->light[c] = fmaf(s->vis, s->global[c], s->local[c]);
     float h[3] = {d[0] + v[0], d[1] + v[1], d[2] + v[2]};
     s->half_norm = fmaxf(sqrtf(dot3(h, h)), 0.0000001f);
     for (int c = 0; c < 3; ++c) s->half[c] = h[c] / s->half_norm;
@@ -1164,12 +1166,13 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             float dglob[3], dvis_s = 0;
             for (int c = 0; c < 3; ++c) dglob[c] = dli[c] * s.vis;
             for (int c = 0; c < 3; ++c) dvis_s += dli[c] * s.global[c];
-            for (int i = 0; i < S_vis; ++i) d_vis[(size_t)idx * S_vis + i] += dvis_s * coef[i];
+            for (int i = 0; i < S_vis; ++i) d_vis[(size_t)idx * S_vis + i] = fmaf(dvis_s, coef[i], d_vis[(size_t)idx * S_vis + i]);
             /* clamp checks after fmaxf never fire (render_equation.cu:440-449, bug-compatible) */
             for (int i = 0; i < S_dir && i < 16; ++i)
-                for (int c = 0; c < 3; ++c) ddir_acc[i * 3 + c] += (double)(dglob[c] * coef[i]);
+                for (int c = 0; c < 3; ++c) ddir_acc[i * 3 + c] += (double)dglob[c] * (double)coef[i];
             for (int i = 0; i < S_dir; ++i) /* loop bound S_direct, render_equation.cu:450 */
-                for (int c = 0; c < 3; ++c) d_inc[((size_t)idx * S_inc + i) * 3 + c] += dli[c] * coef[i];
+                for (int c = 0; c < 3; ++c)
+                    d_inc[((size_t)idx * S_inc + i) * 3 + c] = fmaf(dli[c], coef[i], d_inc[((size_t)idx * S_inc + i) * 3 + c]);
             for (int c = 0; c < 3; ++c) {
                 d_view[3 * idx + c] += dv[c];
                 d_normal[3 * idx + c] += dn[c];

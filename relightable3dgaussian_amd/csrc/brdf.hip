@@ -70,11 +70,15 @@ __device__ __forceinline__ void eval_lights(const float* coef, const float* inc,
     if constexpr (NI > 0) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            lx += inc[3 * i] * coef[i]; ly += inc[3 * i + 1] * coef[i]; lz += inc[3 * i + 2] * coef[i];
+            lx = __builtin_fmaf(inc[3 * i], coef[i], lx);
+            ly = __builtin_fmaf(inc[3 * i + 1], coef[i], ly);
+            lz = __builtin_fmaf(inc[3 * i + 2], coef[i], lz);
         }
     } else {
         for (int i = 0; i < S_inc; ++i) {
-            lx += inc[3 * i] * coef[i]; ly += inc[3 * i + 1] * coef[i]; lz += inc[3 * i + 2] * coef[i];
+            lx = __builtin_fmaf(inc[3 * i], coef[i], lx);
+            ly = __builtin_fmaf(inc[3 * i + 1], coef[i], ly);
+            lz = __builtin_fmaf(inc[3 * i + 2], coef[i], lz);
         }
     }
     s.local[0] = fmaxf(lx, 0.0f); s.local[1] = fmaxf(ly, 0.0f); s.local[2] = fmaxf(lz, 0.0f);
@@ -82,26 +86,33 @@ __device__ __forceinline__ void eval_lights(const float* coef, const float* inc,
     if constexpr (ND > 0) {
 #pragma unroll
         for (int i = 0; i < ND; ++i) {
-            gx += dir[3 * i] * coef[i]; gy += dir[3 * i + 1] * coef[i]; gz += dir[3 * i + 2] * coef[i];
+            gx = __builtin_fmaf(dir[3 * i], coef[i], gx);
+            gy = __builtin_fmaf(dir[3 * i + 1], coef[i], gy);
+            gz = __builtin_fmaf(dir[3 * i + 2], coef[i], gz);
         }
     } else {
         for (int i = 0; i < S_dir; ++i) {
-            gx += dir[3 * i] * coef[i]; gy += dir[3 * i + 1] * coef[i]; gz += dir[3 * i + 2] * coef[i];
+            gx = __builtin_fmaf(dir[3 * i], coef[i], gx);
+            gy = __builtin_fmaf(dir[3 * i + 1], coef[i], gy);
+            gz = __builtin_fmaf(dir[3 * i + 2], coef[i], gz);
         }
     }
     s.global[0] = fmaxf(gx, 0.0f); s.global[1] = fmaxf(gy, 0.0f); s.global[2] = fmaxf(gz, 0.0f);
     float vv = 0.5f;
     if constexpr (NV > 0) {
 #pragma unroll
-        for (int i = 0; i < NV; ++i) vv += vis[i] * coef[i];
+        for (int i = 0; i < NV; ++i) vv = __builtin_fmaf(vis[i], coef[i], vv);
     } else {
-        for (int i = 0; i < S_vis; ++i) vv += vis[i] * coef[i];
+        for (int i = 0; i < S_vis; ++i) vv = __builtin_fmaf(vis[i], coef[i], vv);
     }
     s.vis = fmaxf(0.0f, fminf(vv, 1.0f));
 #pragma unroll
-    for (int c = 0; c < 3; ++c) s.light[c] = s.vis * s.global[c] + s.local[c];
+    for (int c = 0; c < 3; ++c) s.light[c] = __builtin_fmaf(s.vis, s.global[c], s.local[c]);
 }
 
+// The SH light sums (render_equation.cu:118-136), their backward accumulations (:436-452) and the
+// light composition are explicit fmaf chains in sample / coefficient order, as the oracle's (what
+// nvcc's default contraction makes of the reference's `+= a * b` loops, and one instruction each).
 // render_equation.cu:138-161 for one sample, with the per-Gaussian terms (amp, sharp, r2v, the
 // view-side GGX factor g2 = 0.5 / denom2) hoisted by the caller -- the same IEEE operations in the
 // same order as the oracle's brdf_eval (true divisions, FP contraction off for this file), so D,
@@ -408,28 +419,28 @@ brdf_bwd_kernel(BrdfKArgs a) {
             const float dvis_s = dli[0] * s.global[0] + dli[1] * s.global[1] + dli[2] * s.global[2];
             if constexpr (NV > 0) {
 #pragma unroll
-                for (int i = 0; i < NV; ++i) dvis_r[i] += dvis_s * coef[i];
+                for (int i = 0; i < NV; ++i) dvis_r[i] = __builtin_fmaf(dvis_s, coef[i], dvis_r[i]);
             } else {
-                for (int i = 0; i < in.S_visibility; ++i) dvis_g[i] += dvis_s * coef[i];
+                for (int i = 0; i < in.S_visibility; ++i) dvis_g[i] = __builtin_fmaf(dvis_s, coef[i], dvis_g[i]);
             }
 #pragma unroll
             for (int i = 0; i < NDA; ++i)
                 if (i < S_dir) {
-                    ddir[3 * i] += dglob[0] * coef[i];
-                    ddir[3 * i + 1] += dglob[1] * coef[i];
-                    ddir[3 * i + 2] += dglob[2] * coef[i];
+                    ddir[3 * i] = __builtin_fmaf(dglob[0], coef[i], ddir[3 * i]);
+                    ddir[3 * i + 1] = __builtin_fmaf(dglob[1], coef[i], ddir[3 * i + 1]);
+                    ddir[3 * i + 2] = __builtin_fmaf(dglob[2], coef[i], ddir[3 * i + 2]);
                 }
             if constexpr (NI > 0) {
 #pragma unroll
                 for (int i = 0; i < NI; ++i)
                     if (i < n_inc_upd) {
-                        dinc_r[3 * i] += dli[0] * coef[i];
-                        dinc_r[3 * i + 1] += dli[1] * coef[i];
-                        dinc_r[3 * i + 2] += dli[2] * coef[i];
+                        dinc_r[3 * i] = __builtin_fmaf(dli[0], coef[i], dinc_r[3 * i]);
+                        dinc_r[3 * i + 1] = __builtin_fmaf(dli[1], coef[i], dinc_r[3 * i + 1]);
+                        dinc_r[3 * i + 2] = __builtin_fmaf(dli[2], coef[i], dinc_r[3 * i + 2]);
                     }
             } else {
                 for (int i = 0; i < n_inc_upd; ++i)
-                    for (int c = 0; c < 3; ++c) dinc_g[3 * i + c] += dli[c] * coef[i];
+                    for (int c = 0; c < 3; ++c) dinc_g[3 * i + c] = __builtin_fmaf(dli[c], coef[i], dinc_g[3 * i + c]);
             }
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
