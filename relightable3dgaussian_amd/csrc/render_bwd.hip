@@ -337,34 +337,6 @@ __device__ __forceinline__ void split_bf16x2(const float (&x)[8], bf16x8& h, bf1
 #ifndef R3DG_BWDG_NB
 #define R3DG_BWDG_NB 64  // instances per staged batch of the DMA-staged kernel
 #endif
-#ifndef R3DG_BWD_LDSIDS
-#define R3DG_BWD_LDSIDS 0  // 1: the next batches' Gaussian ids and contribution bytes come by LDS-DMA
-                           // too, so no compiler-tracked load is pending in the batch loop and the
-                           // batch-end wait skips the flush's younger atomics / row stores
-#endif
-
-// s_waitcnt vmcnt(4 q) for a wave-uniform q (immediates only): waits for every vector-memory
-// operation of this wave except its 4 q youngest
-__device__ __forceinline__ void wait_vmcnt_except4(int q) {
-    switch (q) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-        case 7: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
-        case 8: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-        case 9: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
-        case 10: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
-        case 11: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
-        case 12: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
-        case 13: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
-        case 14: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
-    }
-}
 #ifndef R3DG_BWDG_GRP
 #define R3DG_BWDG_GRP 13  // instances per MFMA group of the DMA-staged kernel (64 / 13 measured best of
                           // 32 / 16, 64 / 12, 64 / 13, 32 / 12: the smaller w|q image buys the larger batch)
@@ -407,13 +379,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     // unrelated LDS reads): [w|q images | 2 staging buffers | max_last]. With GRP < 16 the MFMA's
     // A reads of rows GRP..15 run past a wave's image into the next image or the staging buffer
     // (valid LDS, values ignored: those D rows are never stored).
-    // (+ with R3DG_BWD_LDSIDS: Gaussian ids [2][NB] and contribution-byte words [2][20] of the
-    // batches being staged)
-    constexpr int IDS4 = R3DG_BWD_LDSIDS ? (2 * NB + 2 * 20 + 3) / 4 : 0;
-    __shared__ float4 s_lds[NW * WQF4 + 2 * SBUF + 1 + IDS4];
+    __shared__ float4 s_lds[NW * WQF4 + 2 * SBUF + 1];
     float4* const stage = s_lds + NW * WQF4;
-    uint32_t* const s_gid = reinterpret_cast<uint32_t*>(stage + 2 * SBUF + 1);  // [2][NB]
-    uint32_t* const s_cbw = s_gid + 2 * NB;                                     // [2][20]
 
     const int tile = block_tile(a.tile_order, a.num_tiles);
     const int w = threadIdx.x >> 6;
@@ -661,33 +628,6 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     auto batch_bits = [&](int hi_b) -> uint32_t {
         return l < min(NB, hi_b) ? (uint32_t)a.contrib[range.x + (uint32_t)(hi_b - 1 - l)] : 0u;
     };
-    // R3DG_BWD_LDSIDS: the ids of the batch ending at hi_b into s_gid[p] (wave 0, one dword per lane,
-    // tail lanes clamped as batch_gid) and the words holding its contribution bytes into s_cbw[p]
-    // (wave 1: the <= 17 aligned words covering positions [first, last])
-    auto dma_dword = [&](const void* src, uint32_t lds_off) {
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + lds_off);
-        int keep;
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-    };
-    const uint32_t ids_off = (uint32_t)((NW * WQF4 + 2 * SBUF + 1) * 16);
-    auto dma_gids = [&](int hi_b, int p) {
-        if (w != 0) return;  // wave-uniform
-        const int tt = min(l, min(NB, hi_b) - 1);
-        dma_dword(a.point_list + range.x + (uint32_t)(hi_b - 1 - tt), ids_off + (uint32_t)(p * NB * 4));
-    };
-    auto dma_bits = [&](int hi_b, int p) {
-        if (w != 1 % NW) return;  // wave-uniform
-        const uint32_t last = range.x + (uint32_t)(hi_b - 1), first = range.x + (uint32_t)(hi_b - min(NB, hi_b));
-        const uint32_t a0 = first & ~3u;
-        if (l <= (int)((last - a0) >> 2))
-            dma_dword(a.contrib + a0 + 4 * l, ids_off + (uint32_t)((2 * NB + p * 20) * 4));
-    };
-    auto lds_bits = [&](int hi_b, int p) -> uint32_t {
-        const uint32_t last = range.x + (uint32_t)(hi_b - 1), first = range.x + (uint32_t)(hi_b - min(NB, hi_b));
-        const uint8_t* b = reinterpret_cast<const uint8_t*>(s_cbw + p * 20);
-        return l < min(NB, hi_b) ? (uint32_t)b[last - (uint32_t)l - (first & ~3u)] : 0u;
-    };
     int r = 0;
     uint32_t gid_cur = max_last > 0 ? batch_gid(max_last) : 0u;  // Gaussian of instance l of the current batch
     if (max_last > 0) issue(gid_cur, 0);
@@ -700,32 +640,19 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     const long long t_begin = wall_clock64();
     long long t_wait = 0, t_mask = 0;
 #endif
-    int nflush = 0;  // flushes since this batch's DMA issue (R3DG_BWD_LDSIDS batch-end wait)
     for (int hi = max_last; hi > 0; hi -= NB) {
         const int cnt = min(NB, hi);
         const int hn = hi - NB;
 #ifdef R3DG_EXP_COUNT
         const long long tm0 = wall_clock64();
 #endif
-#if R3DG_BWD_LDSIDS
-        if (hi != max_last) {  // landed before the barrier that ended the previous batch
-            cb_next = lds_bits(hi, buf);
-            gid_next = hn > 0 ? s_gid[buf * NB + l] : 0u;
-        }
-#endif
         const uint32_t cbits = cb_next;
         const uint32_t gid_staged = gid_next;
         if (hn > 0) {  // block-uniform: stage the next batch while this one blends
             issue(gid_next, buf ^ 1);
-#if R3DG_BWD_LDSIDS
-            if (hn > NB) dma_gids(hn - NB, buf ^ 1);
-            dma_bits(hn, buf ^ 1);
-#else
             gid_next = hn > NB ? batch_gid(hn - NB) : 0u;
             cb_next = batch_bits(hn);
-#endif
         }
-        nflush = 0;
         st = stage + buf * SBUF;
         // this wave's live instances: the forward's contribution bits for its quadrant (lanes
         // 0..cnt-1; zero past the batch)
@@ -805,7 +732,6 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             if (r > GRP - 2) {
                 flush(r);
                 r = 0;
-                ++nflush;
             }
         }
         // the next batch's records have landed (this wave's DMA) and every wave is done with
@@ -813,13 +739,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #ifdef R3DG_EXP_COUNT
         const long long tw0 = wall_clock64();
 #endif
-#if R3DG_BWD_LDSIDS
-        // this wave's DMA (records, ids, bits) is older than every flush's (NXB + 1) * 4 atomic adds
-        // / row stores (r >= 12 there: every one of them issues), so those may stay in flight
-        wait_vmcnt_except4(min(nflush * (NXB + 1), 15));
-#else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         __syncthreads();
 #ifdef R3DG_EXP_COUNT
         t_wait += wall_clock64() - tw0;

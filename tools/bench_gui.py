@@ -6,8 +6,8 @@ own textures (tests/golden/textures.npz), and three forward variants:
   default   all-default shader managers (the fused default path, render_fwd_glds_kernel);
   shaders   every Gaussian in a non-default SH shader bucket and a non-default splat shader bucket
             (random ids, seed 0): working copies, sh_shader_kernel<ID> per bucket, the
-            intermediate depth / stencil pass, splat_shader_kernel<ID> per bucket,
-            render_fwd_shader_kernel;
+            intermediate depth / stencil pass (intermediate_glds_kernel), splat_shader_kernel<ID> per
+            bucket, shader_record_kernel, render_fwd_glds_kernel<SHADER=true>;
   gui       `shaders` + the post-process list [QuantizeLighting, SobelFilter, Invert].
 Median of --iters forward calls after warmup, HIP events on the current stream. Run it under
 `rocprofv3 --kernel-trace --stats` for the per-kernel split.
