@@ -263,6 +263,23 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
     return (int)(threadIdx.x & 63) == lane ? x : v;
 }
 
+// Lane that holds MFMA-group row r's bookkeeping (its partial row / Gaussian, mean offset): lane
+// i = r & 3 of 16-lane row r >> 2. The flush's lane group g (lanes 16g..16g+15) handles D row
+// 4g + i of accumulator element i, so row_bcast(v, i) -- DPP row_newbcast:i, one VALU, no LDS --
+// hands every lane of the group its row's value.
+__device__ __forceinline__ int row_lane(int r) { return 16 * (r >> 2) + (r & 3); }
+__device__ __forceinline__ int row_bcast(int v, int i) {
+    switch (i) {  // the DPP control must be an immediate (i is a constant after unrolling)
+        case 0: return __builtin_amdgcn_update_dpp(0, v, 0x150, 0xf, 0xf, false);
+        case 1: return __builtin_amdgcn_update_dpp(0, v, 0x151, 0xf, 0xf, false);
+        case 2: return __builtin_amdgcn_update_dpp(0, v, 0x152, 0xf, 0xf, false);
+        default: return __builtin_amdgcn_update_dpp(0, v, 0x153, 0xf, 0xf, false);
+    }
+}
+__device__ __forceinline__ float row_bcast(float v, int i) {
+    return __int_as_float(row_bcast(__float_as_int(v), i));
+}
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // Exact bf16 splits by truncation: h = the top 8 significant bits of x (its upper 16 bits), r = x - h
@@ -436,8 +453,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     }
     float u = 0.f;
     const float TFB = T_final * bg_dot;
-    int rowj = 0;  // group row r's partial-row index (4 * slot + quadrant) in lane r (ATOM: its Gaussian)
-    float d0xr = 0.f, d0yr = 0.f;  // ATOM: group row r's mean - quadrant centre in lane r
+    int rowj = 0;  // group row r's partial-row index (4 * slot + quadrant) in lane row_lane(r) (ATOM: its Gaussian)
+    float d0xr = 0.f, d0yr = 0.f;  // ATOM: group row r's mean - quadrant centre in lane row_lane(r)
     const float qcx = (float)(tx * kTileX + (w & 1) * 8) + 3.5f, qcy = (float)(ty * kTileY + (w >> 1) * 8) + 3.5f;
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
     const int max_last = block_max_last(wmax, s_max_last);
@@ -556,24 +573,28 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int row = (l >> 4) * 4 + i;
-                const uint32_t gid = (uint32_t)__shfl(rowj, row);
-                const float d0x = __shfl(d0xr, row), d0y = __shfl(d0yr, row);
+                const uint32_t gid = (uint32_t)row_bcast(rowj, i);
+                const float d0x = row_bcast(d0xr, i), d0y = row_bcast(d0yr, i);
                 // the row's moments about the quadrant centre, S0 / Sx / Sy from lanes 0..2 of the row
-                const float s0 = __shfl(accY[i], l & 48), s1 = __shfl(accY[i], (l & 48) + 1),
-                            s2 = __shfl(accY[i], (l & 48) + 2);
+                const float s0 = row_bcast(accY[i], 0), s1 = row_bcast(accY[i], 1), s2 = row_bcast(accY[i], 2);
                 if (row < r) {
                     float* dst = a.sums + (size_t)gid * a.SRS;
 #pragma unroll
                     for (int xb = 0; xb < NXB; ++xb)
                         if (xb * 16 + nch < 4 + S) atomicAdd(dst + xb * 16 + nch, accX[xb][i]);
                     // expand_moments, one output per lane (the same operations as row_sum_kernel's)
+                    // (every candidate computed and selected: the lanes of a row take all six branches)
                     const float sk = accY[i];
+                    const float e1 = d0x * s0 - s1, e2 = d0y * s0 - s2;
+                    const float e3 = d0x * d0x * s0 - 2.f * d0x * s1 + sk;
+                    const float e4 = d0x * d0y * s0 - d0x * s2 - d0y * s1 + sk;
+                    const float e5 = d0y * d0y * s0 - 2.f * d0y * s2 + sk;
                     float e = s0;
-                    if (nch == 1) e = d0x * s0 - s1;
-                    else if (nch == 2) e = d0y * s0 - s2;
-                    else if (nch == 3) e = d0x * d0x * s0 - 2.f * d0x * s1 + sk;
-                    else if (nch == 4) e = d0x * d0y * s0 - d0x * s2 - d0y * s1 + sk;
-                    else if (nch == 5) e = d0y * d0y * s0 - 2.f * d0y * s2 + sk;
+                    e = nch == 1 ? e1 : e;
+                    e = nch == 2 ? e2 : e;
+                    e = nch == 3 ? e3 : e;
+                    e = nch == 4 ? e4 : e;
+                    e = nch == 5 ? e5 : e;
                     if (nch < 6) atomicAdd(dst + XW + nch, e);
                 }
             }
@@ -583,7 +604,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = (l >> 4) * 4 + i;
-            const uint32_t base = (uint32_t)__shfl(rowj, row);
+            const uint32_t base = (uint32_t)row_bcast(rowj, i);
             if (row < r) {
                 // 32-bit offset in float4 units (RS is a multiple of 8 floats): 4L rows x RS / 4
                 // stay below 2^32 (checked on the host: L * RS < 2^32, L < 178M at S <= 12)
@@ -712,20 +733,20 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 float* wr = wq + r * WQS + l;
                 wr[0] = wv0;
                 wr[GRP * WQS] = qv0;
-                rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j0), r);
+                rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j0), row_lane(r));
                 if constexpr (ATOM) {
-                    d0xr = l == r ? xy0.x - qcx : d0xr;
-                    d0yr = l == r ? xy0.y - qcy : d0yr;
+                    d0xr = l == row_lane(r) ? xy0.x - qcx : d0xr;
+                    d0yr = l == row_lane(r) ? xy0.y - qcy : d0yr;
                 }
             }
             if (has1) {
                 float* wr = wq + (r + 1) * WQS + l;
                 wr[0] = wv1;
                 wr[GRP * WQS] = qv1;
-                rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j1), r + 1);
+                rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j1), row_lane(r + 1));
                 if constexpr (ATOM) {
-                    d0xr = l == r + 1 ? xy1.x - qcx : d0xr;
-                    d0yr = l == r + 1 ? xy1.y - qcy : d0yr;
+                    d0xr = l == row_lane(r + 1) ? xy1.x - qcx : d0xr;
+                    d0yr = l == row_lane(r + 1) ? xy1.y - qcy : d0yr;
                 }
             }
             r += has1 ? 2 : 1;
