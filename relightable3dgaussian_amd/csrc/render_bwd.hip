@@ -659,7 +659,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     int buf = 0;
 #ifdef R3DG_EXP_COUNT
     const long long t_begin = wall_clock64();
-    long long t_wait = 0, t_mask = 0;
+    long long t_wait = 0, t_mask = 0, t_flush = 0;
 #endif
     for (int hi = max_last; hi > 0; hi -= NB) {
         const int cnt = min(NB, hi);
@@ -751,7 +751,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             }
             r += has1 ? 2 : 1;
             if (r > GRP - 2) {
+#ifdef R3DG_EXP_COUNT
+                const long long tf0 = wall_clock64();
+#endif
                 flush(r);
+#ifdef R3DG_EXP_COUNT
+                t_flush += wall_clock64() - tf0;
+#endif
                 r = 0;
             }
         }
@@ -774,6 +780,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         R3DG_EXP_ADD(2, t_wait);                    // batch-end DMA wait + barrier, per wave
         R3DG_EXP_ADD(3, wall_clock64() - t_begin);  // batch loop total, per wave
         R3DG_EXP_ADD(4, t_mask);                    // DMA issue + live masks, per wave
+        R3DG_EXP_ADD(7, t_flush);                   // in-loop flushes, per wave
     }
 #endif
 }

@@ -20,6 +20,7 @@ for i, n in enumerate(names):
     print(f"{n}: {buf[i]}")
 print(f"bwd staging fraction: {buf[2] / max(buf[3], 1):.3f}")
 print(f"bwd mask/issue ticks: {buf[4]} ({buf[4] / max(buf[3], 1):.3f})")
+print(f"bwd in-loop flush ticks: {buf[7]} ({buf[7] / max(buf[3], 1):.3f})")
 # bench.main runs the warm-up steps, the timed steps and as many profiled steps: 2 at --steps 1
 print("m1 steps run: 2")
 print(f"fwd steps done: {fb[2]}\nfwd live pairs (pre-exit): {fb[3]}")
