@@ -257,7 +257,11 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 const float2 xy1 = *reinterpret_cast<const float2*>(st + NB + u1);
                 const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
                 const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
+#ifdef R3DG_FWD_EXP1  // A/B: two scalar exp chains instead of the packed pair (same bits)
+                const f32x2 G = {r3dg_expf(pw0), r3dg_expf(pw1)};
+#else
                 const f32x2 G = r3dg_expf2(pw0, pw1);
+#endif
                 step(j0, true, co0.w, pw0, G.x);
                 step(j1, has1, co1.w, pw1, G.y);
                 if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);

@@ -29,7 +29,7 @@ for part in "$@"; do
       bash tools/pmc_passes.sh
       python tools/pmc_summary.py gpurun_out/pmc > $OUT/pmc_summary.json
       python tools/make_traffic.py $OUT/pmc_summary.json profiles/traffic_latest.json "M1 P=1000000" > /dev/null
-      python tools/make_valu.py $OUT/pmc_summary.json profiles/r04/valu_count_from_r03.txt profiles/valu_latest.json > /dev/null
+      python tools/make_valu.py $OUT/pmc_summary.json profiles/valu_count_latest.txt profiles/valu_latest.json > /dev/null
       cp profiles/traffic_latest.json profiles/valu_latest.json $OUT/ ;;
     ab:*)
       specs=${part#ab:}
