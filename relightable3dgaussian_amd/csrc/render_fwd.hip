@@ -26,7 +26,7 @@ R3DG_EXP_READER(r3dg_exp_counters_fwd)
 #endif
 
 #ifndef R3DG_FWD_WAVES
-#define R3DG_FWD_WAVES 6  // waves per SIMD the register allocation targets (SMAX <= 12)
+#define R3DG_FWD_WAVES 8  // waves per SIMD the register allocation targets (SMAX <= 12): 64 VGPR
 #endif
 
 // ---------------------------------------------------------------------------------------------
@@ -49,7 +49,8 @@ R3DG_EXP_READER(r3dg_exp_counters_fwd)
 // features] (RenderFwdArgs::shader_rec, NA4 float4 per Gaussian, the attribute row's layout) -- the
 // same DMA staging, cull, step and contribution bits as the default path.
 template <int SMAX, bool SHADER>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_FWD_WAVES : 1)))
+// (SMAX = 0 keeps the 6-wave target: at 8 the compiler spills 14 SGPRs)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX == 0 ? 6 : SMAX <= 12 ? R3DG_FWD_WAVES : 1)))
 render_fwd_glds_kernel(RenderFwdArgs a) {
     constexpr int NB = R3DG_FWDG_NB;
     constexpr int NH = NB / 64;                // staged instances per lane
@@ -257,11 +258,9 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 const float2 xy1 = *reinterpret_cast<const float2*>(st + NB + u1);
                 const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
                 const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
-#ifdef R3DG_FWD_EXP1  // A/B: two scalar exp chains instead of the packed pair (same bits)
+                // two scalar exp chains, interleaved by the scheduler (the packed pair, r3dg_expf2,
+                // needs an s_nop between its dependent v_pk_fma_f32: 0.3 % slower at M1)
                 const f32x2 G = {r3dg_expf(pw0), r3dg_expf(pw1)};
-#else
-                const f32x2 G = r3dg_expf2(pw0, pw1);
-#endif
                 step(j0, true, co0.w, pw0, G.x);
                 step(j1, has1, co1.w, pw1, G.y);
                 if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
