@@ -951,12 +951,14 @@ static void fib_dir(const float* n, int ray, int Ns, float rand01, int use_rand,
     float zs[3] = {x, y, z};
     const float v1 = -n[1], v2 = n[0], v3 = 0.f;
     const float v11 = v1 * v1, v22 = v2 * v2, v33 = v3 * v3, v12 = v1 * v2, v13 = v1 * v3, v23 = v2 * v3;
-    const float cp1 = fmaxf(n[2] + 1, 0.0000001f);
-    float o[3] = {(1 + (-v33 - v22) / cp1) * zs[0] + (-v3 + v12 / cp1) * zs[1] + (v2 + v13 / cp1) * zs[2],
-                  (v3 + v12 / cp1) * zs[0] + (1 + (-v33 - v11) / cp1) * zs[1] + (-v1 + v23 / cp1) * zs[2],
-                  (-v2 + v13 / cp1) * zs[0] + (v1 + v23 / cp1) * zs[1] + (1 + (-v22 - v11) / cp1) * zs[2]};
-    const float norm = sqrtf(fmaxf(0.0000001f, o[0] * o[0] + o[1] * o[1] + o[2] * o[2]));
-    dir[0] = o[0] / norm; dir[1] = o[1] / norm; dir[2] = o[2] / norm;
+    /* one division by cp1 and one by norm, then products with the reciprocals (brdf.hip fib_dir; the
+     * reference divides each term, render_equation.cu:104-112: within an ulp) */
+    const float cp1 = fmaxf(n[2] + 1, 0.0000001f), rc = 1.0f / cp1;
+    float o[3] = {(1 + (-v33 - v22) * rc) * zs[0] + (-v3 + v12 * rc) * zs[1] + (v2 + v13 * rc) * zs[2],
+                  (v3 + v12 * rc) * zs[0] + (1 + (-v33 - v11) * rc) * zs[1] + (-v1 + v23 * rc) * zs[2],
+                  (-v2 + v13 * rc) * zs[0] + (v1 + v23 * rc) * zs[1] + (1 + (-v22 - v11) * rc) * zs[2]};
+    const float norm = sqrtf(fmaxf(0.0000001f, o[0] * o[0] + o[1] * o[1] + o[2] * o[2])), rn = 1.0f / norm;
+    dir[0] = o[0] * rn; dir[1] = o[1] * rn; dir[2] = o[2] * rn;
 }
 
 typedef struct {
@@ -986,7 +988,8 @@ static void brdf_eval(int idx, int S_inc, int S_dir, int S_vis, const float* bas
     for (int c = 0; c < 3; ++c) s->light[c] = fmaf(s->vis, s->global[c], s->local[c]);
     float h[3] = {d[0] + v[0], d[1] + v[1], d[2] + v[2]};
     s->half_norm = fmaxf(sqrtf(dot3(h, h)), 0.0000001f);
-    for (int c = 0; c < 3; ++c) s->half[c] = h[c] / s->half_norm;
+    const float rh = 1.0f / s->half_norm;
+    for (int c = 0; c < 3; ++c) s->half[c] = h[c] * rh;
     s->hdn = fmaxf(dot3(s->half, n), 0.0f);
     s->hdo = fmaxf(dot3(s->half, v), 0.0f);
     s->ndi = fmaxf(dot3(n, d), 0.0f);
@@ -1162,7 +1165,8 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             if (s.hdo > 0.0f) for (int c = 0; c < 3; ++c) { dhalf[c] += v[c] * dhdo; dv[c] += s.half[c] * dhdo; }
             if (s.ndi > 0.0f) for (int c = 0; c < 3; ++c) dn[c] += d[c] * dndi;
             if (s.ndo > 0.0f) for (int c = 0; c < 3; ++c) { dn[c] += v[c] * dndo; dv[c] += n[c] * dndo; }
-            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] / s.half_norm;
+            const float rh = 1.0f / s.half_norm;
+            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] * rh;
             float dglob[3], dvis_s = 0;
             for (int c = 0; c < 3; ++c) dglob[c] = dli[c] * s.vis;
             for (int c = 0; c < 3; ++c) dvis_s += dli[c] * s.global[c];

@@ -41,12 +41,15 @@ __device__ __forceinline__ float3 fib_dir(float3 n, int ray, int Ns, float rot) 
     const float y = cs * rad, x = sn * rad;
     const float v1 = -n.y, v2 = n.x, v3 = 0.f;
     const float v11 = v1 * v1, v22 = v2 * v2, v33 = v3 * v3, v12 = v1 * v2, v13 = v1 * v3, v23 = v2 * v3;
-    const float cp1 = fmaxf(n.z + 1, 0.0000001f);
-    const float ox = (1 + (-v33 - v22) / cp1) * x + (-v3 + v12 / cp1) * y + (v2 + v13 / cp1) * z;
-    const float oy = (v3 + v12 / cp1) * x + (1 + (-v33 - v11) / cp1) * y + (-v1 + v23 / cp1) * z;
-    const float oz = (-v2 + v13 / cp1) * x + (v1 + v23 / cp1) * y + (1 + (-v22 - v11) / cp1) * z;
-    const float norm = sqrtf(fmaxf(0.0000001f, ox * ox + oy * oy + oz * oz));
-    return make_float3(ox / norm, oy / norm, oz / norm);
+    // the reference divides six times by cp1 and three times by norm (render_equation.cu:104-112);
+    // here (and in the oracle) one IEEE division each and products with the reciprocal: within an
+    // ulp of the quotients, 7 divisions (~10 VALU each) fewer per sample
+    const float cp1 = fmaxf(n.z + 1, 0.0000001f), rc = 1.0f / cp1;
+    const float ox = (1 + (-v33 - v22) * rc) * x + (-v3 + v12 * rc) * y + (v2 + v13 * rc) * z;
+    const float oy = (v3 + v12 * rc) * x + (1 + (-v33 - v11) * rc) * y + (-v1 + v23 * rc) * z;
+    const float oz = (-v2 + v13 * rc) * x + (v1 + v23 * rc) * y + (1 + (-v22 - v11) * rc) * z;
+    const float norm = sqrtf(fmaxf(0.0000001f, ox * ox + oy * oy + oz * oz)), rn = 1.0f / norm;
+    return make_float3(ox * rn, oy * rn, oz * rn);
 }
 
 struct Sample {
@@ -123,7 +126,8 @@ __device__ __forceinline__ void eval_brdf(const GaussBRDF& G, float3 d, float am
                                           Sample& s) {
     const float hx = d.x + G.v.x, hy = d.y + G.v.y, hz = d.z + G.v.z;
     s.half_norm = fmaxf(sqrtf(hx * hx + hy * hy + hz * hz), 0.0000001f);
-    s.half[0] = hx / s.half_norm; s.half[1] = hy / s.half_norm; s.half[2] = hz / s.half_norm;
+    const float rh = 1.0f / s.half_norm;  // one division, three products (as the oracle)
+    s.half[0] = hx * rh; s.half[1] = hy * rh; s.half[2] = hz * rh;
     s.hdn = fmaxf(s.half[0] * G.n.x + s.half[1] * G.n.y + s.half[2] * G.n.z, 0.0f);
     s.hdo = fmaxf(s.half[0] * G.v.x + s.half[1] * G.v.y + s.half[2] * G.v.z, 0.0f);
     s.ndi = fmaxf(G.n.x * d.x + G.n.y * d.y + G.n.z * d.z, 0.0f);
@@ -411,8 +415,9 @@ brdf_bwd_kernel(BrdfKArgs a) {
 #pragma unroll
                 for (int c = 0; c < 3; ++c) { dn[c] += v[c] * dndo; dv[c] += n[c] * dndo; }
             }
+            const float rh = 1.0f / s.half_norm;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] / s.half_norm;
+            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] * rh;
             float dglob[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) dglob[c] = dli[c] * s.vis;
