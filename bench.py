@@ -424,11 +424,13 @@ def main() -> None:
                                   f"all-gather of the 3-float SH colour gradient, SH sum rebuilt per rank; "
                                   f"{args.chunks} chunks overlapped with the gather phase)"},
         "views_per_s": round(world * args.steps / elapsed, 3),
-        # the blend kernels are bound by neither HBM (frac ~0.14) nor VALU issue (valu.frac ~0.4):
+        # the blend kernels are bound by neither HBM (frac ~0.16) nor VALU issue (valu.frac ~0.5):
         # by dependent LDS / exp latency and the batch barrier (DESIGN.md §4 "Can 0.40 be reached")
         "roofline": {"bound": "latency", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "renderCUDA fwd + bwd: render_fwd_glds_kernel + render_bwd_glds_kernel + row_sum_kernel",
+                     "kernel": "renderCUDA fwd + bwd: render_fwd_glds_kernel + render_bwd_glds_kernel + the reduction's "
+                               "second stage (the sums memset with the default atomic flush; row_sum_kernel with "
+                               "R3DG_BWD_REDUCE=rows)",
                      "algorithmic_bytes": bf + bb, "extra_bytes": fused_sort_bytes(L),
                      "extra_bytes_note": "fused per-tile depth sort in the forward (12 B per instance), not in frac",
                      "kernel_ms": round(t_kern * 1e3, 4), "valu": valu},
