@@ -49,6 +49,7 @@ static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
                                0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
                                -0.5900435899266435f};
 static const float PI_F = 3.14159f; /* render_equation.cu uses the literal 3.14159f */
+#define INV_PI_F (1.0f / 3.14159f) /* products in place of per-sample divisions by PI_F (brdf.hip kInvPi) */
 
 /* ------------------------------------------------------------------------------------------ */
 /* small helpers (auxiliary.h:41-132)                                                          */
@@ -941,7 +942,7 @@ static void sh_coef3(const float* d, float* coef)
 static void fib_dir(const float* n, int ray, int Ns, float rand01, int use_rand, float* dir)
 {
     const float delta = PI_F * (3.0f - sqrtf(5.0f));
-    const float z = 1 - 2 * (float)ray / (2 * (float)Ns - 1);
+    const float z = 1 - (float)ray * (2.0f / (2 * (float)Ns - 1));
     const float rad = sqrtf(1 - z * z);
     float theta = delta * ray;
     if (use_rand) theta = rand01 * 2 * PI_F + theta;
@@ -1027,7 +1028,7 @@ void oracle_render_equation_forward(int P, int S_inc, int S_dir, int S_vis, cons
             brdf_sample s;
             brdf_eval(idx, S_inc, S_dir, S_vis, base + 3 * idx, rough[idx], metal[idx], normals + 3 * idx,
                       viewdirs + 3 * idx, inc, dir_shs, vis_shs, d, coef, &s);
-            float tmp = 2.0f * PI_F * s.ndi / (float)Ns;
+            float tmp = s.ndi * (2.0f * PI_F / (float)Ns);
             for (int c = 0; c < 3; ++c) {
                 float tr = s.light[c] * tmp;
                 acc_p[c] += (s.fd[c] + s.fs[c]) * tr;
@@ -1057,7 +1058,7 @@ void oracle_render_equation_forward_complex(int P, int S_inc, int S_dir, int S_v
             brdf_sample s;
             brdf_eval(idx, S_inc, S_dir, S_vis, base + 3 * idx, rough[idx], metal[idx], normals + 3 * idx,
                       viewdirs + 3 * idx, inc, dir_shs, vis_shs, d, coef, &s);
-            float tmp = 2.0f * PI_F * s.ndi / (float)Ns;
+            float tmp = s.ndi * (2.0f * PI_F / (float)Ns);
             size_t w = (size_t)idx * Ns + r;
             for (int c = 0; c < 3; ++c) {
                 float g = s.vis * s.global[c];
@@ -1074,7 +1075,7 @@ void oracle_render_equation_forward_complex(int P, int S_inc, int S_dir, int S_v
             vis[w] = s.vis;
         }
         float av[3];
-        for (int c = 0; c < 3; ++c) av[c] = dl[c] / PI_F + as[c];
+        for (int c = 0; c < 3; ++c) av[c] = dl[c] * INV_PI_F + as[c];
         accum[idx] = (av[0] + av[1] + av[2]) / 3;
         for (int c = 0; c < 3; ++c) {
             pbr[3 * idx + c] = ad[c] + as[c];
@@ -1119,7 +1120,7 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             float den1 = fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f);
             float den2 = fmaxf(s.ndo * (1 - r2v) + r2v, 0.0000001f);
             float g1 = 0.5f / den1, g2 = 0.5f / den2;
-            const float Tn = 2.0f * PI_F * s.ndi / (float)Ns;
+            const float Tn = s.ndi * (2.0f * PI_F / (float)Ns);
             float dfd[3], dfs[3], dli[3], fsum[3];
             for (int c = 0; c < 3; ++c) {
                 fsum[c] = s.fd[c] + s.fs[c];
@@ -1131,8 +1132,8 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             for (int c = 0; c < 3; ++c) dli[c] += gdl[c] * Tn;
             dndi += gdl[0] * (s.light[0] * K) + gdl[1] * (s.light[1] * K) + gdl[2] * (s.light[2] * K);
             float dbase[3];
-            for (int c = 0; c < 3; ++c) dbase[c] = dfd[c] * (1 - metal_i) / PI_F;
-            float dmetal = -(dfd[0] * b[0] + dfd[1] * b[1] + dfd[2] * b[2]) / PI_F;
+            for (int c = 0; c < 3; ++c) dbase[c] = dfd[c] * ((1 - metal_i) / PI_F);
+            float dmetal = -(dfd[0] * b[0] + dfd[1] * b[1] + dfd[2] * b[2]) * INV_PI_F;
             float dD = dfs[0] * s.V * s.F[0] + dfs[1] * s.V * s.F[1] + dfs[2] * s.V * s.F[2];
             float dF[3];
             for (int c = 0; c < 3; ++c) dF[c] = dfs[c] * s.D * s.V;
@@ -1155,7 +1156,7 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             for (int c = 0; c < 3; ++c) dbase[c] += metal_i * dF0[c];
             dmetal += (b[0] - 0.04f) * dF0[0] + (b[1] - 0.04f) * dF0[1] + (b[2] - 0.04f) * dF0[2];
             float dg1 = dV * g2, dg2 = dV * g1;
-            float dden1 = -0.5f / (den1 * den1) * dg1, dden2 = -0.5f / (den2 * den2) * dg2;
+            float dden1 = -2.0f * (g1 * g1) * dg1, dden2 = -0.5f / (den2 * den2) * dg2; /* -0.5/den1^2 = -2 g1^2 */
             dndi = dden1 * (1 - r2v); /* overwrite: render_equation.cu:403 (bug-compatible) */
             float dndo = dden2 * (1 - r2v);
             float dr2v = (1.0f - s.ndi) * dden1 + (1.0f - s.ndo) * dden2;

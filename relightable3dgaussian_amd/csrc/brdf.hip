@@ -18,6 +18,7 @@
 namespace r3dg {
 
 constexpr float kPi = 3.14159f;  // the reference's literal
+constexpr float kInvPi = 1.0f / kPi;  // products in place of per-sample divisions by kPi (as the oracle)
 
 __device__ __forceinline__ void sh_coef16(float x, float y, float z, float* coef) {
     const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
@@ -33,7 +34,7 @@ __device__ __forceinline__ void sh_coef16(float x, float y, float z, float* coef
 
 __device__ __forceinline__ float3 fib_dir(float3 n, int ray, int Ns, float rot) {
     const float delta = kPi * (3.0f - sqrtf(5.0f));
-    const float z = 1 - 2 * (float)ray / (2 * (float)Ns - 1);
+    const float z = 1 - (float)ray * (2.0f / (2 * (float)Ns - 1));  // the quotient hoisted (oracle: same)
     const float rad = sqrtf(1 - z * z);
     const float theta = rot + delta * ray;
     float sn, cs;
@@ -219,7 +220,7 @@ __global__ void __launch_bounds__(256) brdf_fwd_kernel(BrdfKArgs a) {
         else
             eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, in.direct_shs, in.S_direct, vis_g, in.S_visibility, s);
         eval_brdf(G, d, amp, sharp, r2v, g2, s);
-        const float tmp = 2.0f * kPi * s.ndi / (float)Ns;
+        const float tmp = s.ndi * (2.0f * kPi / (float)Ns);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const float tr = s.light[c] * tmp;
@@ -251,7 +252,7 @@ __global__ void __launch_bounds__(256) brdf_fwd_kernel(BrdfKArgs a) {
         const r3dg_brdf_complex_outputs& o = a.cx;
         float av[3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) av[c] = dl[c] / kPi + rs[c];
+        for (int c = 0; c < 3; ++c) av[c] = dl[c] * kInvPi + rs[c];
         o.accum[idx] = (av[0] + av[1] + av[2]) / 3;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -354,7 +355,7 @@ brdf_bwd_kernel(BrdfKArgs a) {
             const float e_amp = s.e_amp;
             const float den1 = fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f);
             const float g1 = 0.5f / den1;
-            const float Tn = 2.0f * kPi * s.ndi / (float)Ns;
+            const float Tn = s.ndi * (2.0f * kPi / (float)Ns);
             float dfd[3], dfs[3], dli[3], fsum[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -368,8 +369,8 @@ brdf_bwd_kernel(BrdfKArgs a) {
             // dL_dn_d_i of :372 / :376 is overwritten at :403 before any use (bug-compatible): not formed
             float dbase[3];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) dbase[c] = dfd[c] * (1 - metal) / kPi;
-            float dmetal = -(dfd[0] * b[0] + dfd[1] * b[1] + dfd[2] * b[2]) / kPi;
+            for (int c = 0; c < 3; ++c) dbase[c] = dfd[c] * ((1 - metal) / kPi);
+            float dmetal = -(dfd[0] * b[0] + dfd[1] * b[1] + dfd[2] * b[2]) * kInvPi;
             const float dD = dfs[0] * s.V * s.F[0] + dfs[1] * s.V * s.F[1] + dfs[2] * s.V * s.F[2];
             float dF[3];
 #pragma unroll
@@ -393,7 +394,8 @@ brdf_bwd_kernel(BrdfKArgs a) {
             for (int c = 0; c < 3; ++c) dbase[c] += metal * dF0[c];
             dmetal += (b[0] - 0.04f) * dF0[0] + (b[1] - 0.04f) * dF0[1] + (b[2] - 0.04f) * dF0[2];
             const float dg1 = dV * g2, dg2 = dV * g1;
-            const float dden1 = -0.5f / (den1 * den1) * dg1, dden2 = -0.5f / (den2 * den2) * dg2;
+            // -0.5 / den1^2 = -2 g1^2 (one division per sample fewer; oracle: same)
+            const float dden1 = -2.0f * (g1 * g1) * dg1, dden2 = -0.5f / (den2 * den2) * dg2;
             const float dndi2 = dden1 * (1 - r2v);
             const float dndo = dden2 * (1 - r2v);
             const float dr2v = (1.0f - s.ndi) * dden1 + (1.0f - s.ndo) * dden2;
@@ -554,7 +556,7 @@ __global__ void __launch_bounds__(256) brdf_fwd_lane_kernel(BrdfKArgs a, int GB)
         else
             eval_lights<0, 0, 0>(coef, inc_g, in.S_incident, in.direct_shs, in.S_direct, vis_g, in.S_visibility, s);
         eval_brdf(G, d, amp, sharp, r2v, g2, s);
-        const float tmp = 2.0f * kPi * s.ndi / (float)Ns;
+        const float tmp = s.ndi * (2.0f * kPi / (float)Ns);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const float tr = s.light[k] * tmp;
@@ -601,7 +603,7 @@ __global__ void __launch_bounds__(256) brdf_fwd_lane_kernel(BrdfKArgs a, int GB)
             const r3dg_brdf_complex_outputs& o = a.cx;
             float av[3];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) av[k] = v[k] / kPi + v[9 + k];
+            for (int k = 0; k < 3; ++k) av[k] = v[k] * kInvPi + v[9 + k];
             o.accum[idx] = (av[0] + av[1] + av[2]) / 3;
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
