@@ -580,8 +580,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 if (row < r) {
                     float* dst = a.sums + (size_t)gid * a.SRS;
 #pragma unroll
+#ifdef R3DG_EXP_ATOMSTORE  // timing experiment only (results invalid): plain stores for the atomics
+#define R3DG_FLUSH_ADD(p, v) (*(p) = (v))
+#else
+#define R3DG_FLUSH_ADD(p, v) atomicAdd((p), (v))
+#endif
                     for (int xb = 0; xb < NXB; ++xb)
-                        if (xb * 16 + nch < 4 + S) atomicAdd(dst + xb * 16 + nch, accX[xb][i]);
+                        if (xb * 16 + nch < 4 + S) R3DG_FLUSH_ADD(dst + xb * 16 + nch, accX[xb][i]);
                     // expand_moments, one output per lane (the same operations as row_sum_kernel's)
                     // (every candidate computed and selected: the lanes of a row take all six branches)
                     const float sk = accY[i];
@@ -595,7 +600,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                     e = nch == 3 ? e3 : e;
                     e = nch == 4 ? e4 : e;
                     e = nch == 5 ? e5 : e;
-                    if (nch < 6) atomicAdd(dst + XW + nch, e);
+                    if (nch < 6) R3DG_FLUSH_ADD(dst + XW + nch, e);
                 }
             }
             wave_lds_sync();
