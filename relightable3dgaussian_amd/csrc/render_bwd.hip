@@ -518,8 +518,9 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         floatx4 accX[NXB], accY = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int xb = 0; xb < NXB; ++xb) accX[xb] = floatx4{0.f, 0.f, 0.f, 0.f};
-        // w rows times the upstream gradients on the bf16 MFMA: w = w1 + w2 + w3 (three terms), X =
-        // X1 + X2; the five products above 2^-24 of w X, smallest first
+        // w rows times the upstream gradients on the bf16 MFMA: X = X1 + X2 (two terms), w = h + m
+        // (R3DG_BWD_SPLIT = 2, default: m rounded to nearest, three products m X1, h X2, h X1) or
+        // w = h + m + o exactly (3: the five products above 2^-24, smallest first)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             const float* src = wq + (l & 15) * WQS + 32 * b + 8 * (l >> 4);
@@ -527,7 +528,14 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) wv[i] = src[i];
             bf16x8 h, m, o;
-#if R3DG_BWD_SPLIT == 2
+#if R3DG_BWD_SPLIT == 1  // timing experiment only (results inexact): one term, one product
+            split_bf16x2(wv, h, m);
+            (void)o;
+            (void)m;
+#pragma unroll
+            for (int xb = 0; xb < NXB; ++xb)
+                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
+#elif R3DG_BWD_SPLIT == 2
             split_bf16x2(wv, h, m);
             (void)o;
 #pragma unroll
@@ -557,7 +565,12 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) qv[i] = src[i];
             bf16x8 h, m, o;
-#if R3DG_BWD_SPLIT_Q == 2
+#if R3DG_BWD_SPLIT_Q == 1  // timing experiment only (results inexact)
+            split_bf16x2(qv, h, m);
+            (void)o;
+            (void)m;
+            accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, yb[b], accY, 0, 0, 0);
+#elif R3DG_BWD_SPLIT_Q == 2
             split_bf16x2(qv, h, m);
             (void)o;
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, yb[b], accY, 0, 0, 0);
@@ -569,6 +582,11 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o, yb[b], accY, 0, 0, 0);
 #endif
         }
+#ifdef R3DG_EXP_NOEPI  // timing experiment only (results invalid): no broadcasts, expansion, stores
+        if (accX[0][0] == 1.2345e-30f && accY[0] == 1.2345e-30f) a.sums[l] = accX[0][1] + accY[1] + accX[0][2] + accY[2];
+        wave_lds_sync();
+        return;
+#endif
         if constexpr (ATOM) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
