@@ -831,8 +831,10 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     }();
     // atomic sums: [X part | 6 moments | pad] per Gaussian, rows of 32 floats (128 B) so each
     // 16-float X segment is one aligned 64-B atomic request
-    int SRS = (RS + 31) & ~31;
-    if (const char* e = getenv("R3DG_BWD_SRS")) SRS = std::max(RS, atoi(e)) & ~7;  // A/B of the sums' row stride
+    // (at least the X part and the 6 moments: XW + 8 floats per row)
+    const int srs_min = 16 * bwd_xblocks(S) + 8;
+    int SRS = (std::max(RS, srs_min) + 31) & ~31;
+    if (const char* e = getenv("R3DG_BWD_SRS")) SRS = std::max(srs_min, atoi(e)) & ~7;  // A/B of the sums' row stride
     const size_t row_bytes = atomic_sums ? 0 : sizeof(float) * (size_t)RS * 4 * L;
     const size_t sum_bytes = sizeof(float) * (size_t)(atomic_sums ? SRS : RS) * P;
     char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + sum_bytes);

@@ -270,10 +270,11 @@ __device__ __forceinline__ int write_lane(int v, int x, int lane) {
 __device__ __forceinline__ int row_lane(int r) { return 16 * (r >> 2) + (r & 3); }
 __device__ __forceinline__ int row_bcast(int v, int i) {
     switch (i) {  // the DPP control must be an immediate (i is a constant after unrolling)
-        case 0: return __builtin_amdgcn_update_dpp(0, v, 0x150, 0xf, 0xf, false);
-        case 1: return __builtin_amdgcn_update_dpp(0, v, 0x151, 0xf, 0xf, false);
-        case 2: return __builtin_amdgcn_update_dpp(0, v, 0x152, 0xf, 0xf, false);
-        default: return __builtin_amdgcn_update_dpp(0, v, 0x153, 0xf, 0xf, false);
+        // (every lane reads a valid source lane: bound_ctrl, no `old` operand to materialise)
+        case 0: return __builtin_amdgcn_mov_dpp(v, 0x150, 0xf, 0xf, true);
+        case 1: return __builtin_amdgcn_mov_dpp(v, 0x151, 0xf, 0xf, true);
+        case 2: return __builtin_amdgcn_mov_dpp(v, 0x152, 0xf, 0xf, true);
+        default: return __builtin_amdgcn_mov_dpp(v, 0x153, 0xf, 0xf, true);
     }
 }
 __device__ __forceinline__ float row_bcast(float v, int i) {
@@ -508,6 +509,9 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         }
     // pad lanes of the moment stores: the quadrant centre (row_sum expands the moments about the mean)
     const float cpad = nch == 6 ? qcx : qcy;
+    // atomic flush: this lane's column of the per-Gaussian sums, and the row stride in bytes
+    float* const lane_sums = a.sums + nch;
+    const uint32_t srs = (uint32_t)a.SRS;
     auto flush = [&](int r) {
         if (l == 0) R3DG_EXP_ADD(1, 1);
 #ifdef R3DG_EXP_NOFLUSH  // timing experiment only (results invalid): no reduction, no rows
@@ -595,31 +599,36 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 const float d0x = row_bcast(d0xr, i), d0y = row_bcast(d0yr, i);
                 // the row's moments about the quadrant centre, S0 / Sx / Sy from lanes 0..2 of the row
                 const float s0 = row_bcast(accY[i], 0), s1 = row_bcast(accY[i], 1), s2 = row_bcast(accY[i], 2);
-                if (row < r) {
-                    float* dst = a.sums + (size_t)gid * a.SRS;
-#pragma unroll
+                // computed by every lane, stored under one lane mask per atomic (no branch around
+                // the expansion); the address is one u32 x u32 product per row. (Adding 0 from the
+                // masked lanes instead measured 23x slower: rows past the group, never written,
+                // all name Gaussian 0, and every wave's zeros contend on its row.)
+                const bool ok = row < r;
+                float* dst = lane_sums + (uint64_t)gid * srs;
 #ifdef R3DG_EXP_ATOMSTORE  // timing experiment only (results invalid): plain stores for the atomics
 #define R3DG_FLUSH_ADD(p, v) (*(p) = (v))
+#elif defined(R3DG_EXP_NOSTORE)  // timing experiment only (results invalid): the epilogue without its stores
+#define R3DG_FLUSH_ADD(p, v) do { if ((v) == 1.2345e-30f) *(p) = 0.f; } while (0)
 #else
 #define R3DG_FLUSH_ADD(p, v) atomicAdd((p), (v))
 #endif
-                    for (int xb = 0; xb < NXB; ++xb)
-                        if (xb * 16 + nch < 4 + S) R3DG_FLUSH_ADD(dst + xb * 16 + nch, accX[xb][i]);
-                    // expand_moments, one output per lane (the same operations as row_sum_kernel's)
-                    // (every candidate computed and selected: the lanes of a row take all six branches)
-                    const float sk = accY[i];
-                    const float e1 = d0x * s0 - s1, e2 = d0y * s0 - s2;
-                    const float e3 = d0x * d0x * s0 - 2.f * d0x * s1 + sk;
-                    const float e4 = d0x * d0y * s0 - d0x * s2 - d0y * s1 + sk;
-                    const float e5 = d0y * d0y * s0 - 2.f * d0y * s2 + sk;
-                    float e = s0;
-                    e = nch == 1 ? e1 : e;
-                    e = nch == 2 ? e2 : e;
-                    e = nch == 3 ? e3 : e;
-                    e = nch == 4 ? e4 : e;
-                    e = nch == 5 ? e5 : e;
-                    if (nch < 6) R3DG_FLUSH_ADD(dst + XW + nch, e);
-                }
+#pragma unroll
+                for (int xb = 0; xb < NXB; ++xb)
+                    if (ok && xb * 16 + nch < 4 + S) R3DG_FLUSH_ADD(dst + xb * 16, accX[xb][i]);
+                // expand_moments, one output per lane (the same operations as row_sum_kernel's)
+                // (every candidate computed and selected: the lanes of a row take all six branches)
+                const float sk = accY[i];
+                const float e1 = d0x * s0 - s1, e2 = d0y * s0 - s2;
+                const float e3 = d0x * d0x * s0 - 2.f * d0x * s1 + sk;
+                const float e4 = d0x * d0y * s0 - d0x * s2 - d0y * s1 + sk;
+                const float e5 = d0y * d0y * s0 - 2.f * d0y * s2 + sk;
+                float e = s0;
+                e = nch == 1 ? e1 : e;
+                e = nch == 2 ? e2 : e;
+                e = nch == 3 ? e3 : e;
+                e = nch == 4 ? e4 : e;
+                e = nch == 5 ? e5 : e;
+                if (ok && nch < 6) R3DG_FLUSH_ADD(dst + XW, e);
             }
             wave_lds_sync();
             return;
