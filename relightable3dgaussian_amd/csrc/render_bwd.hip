@@ -352,6 +352,14 @@ __device__ __forceinline__ void split_bf16x2(const float (&x)[8], bf16x8& h, bf1
     m = M.v;
 }
 
+// the atomic flush's add (timing-only builds swap it: tools/exp_build.sh)
+#ifdef R3DG_EXP_ATOMSTORE  // timing experiment only (results invalid): plain stores for the atomics
+#define R3DG_FLUSH_ADD(p, v) (*(p) = (v))
+#elif defined(R3DG_EXP_NOSTORE)  // timing experiment only (results invalid): the epilogue without its stores
+#define R3DG_FLUSH_ADD(p, v) do { if ((v) == 1.2345e-30f) *(p) = 0.f; } while (0)
+#else
+#define R3DG_FLUSH_ADD(p, v) atomicAdd((p), (v))
+#endif
 #ifndef R3DG_BWDG_NB
 #define R3DG_BWDG_NB 64  // instances per staged batch of the DMA-staged kernel
 #endif
@@ -605,13 +613,6 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 // all name Gaussian 0, and every wave's zeros contend on its row.)
                 const bool ok = row < r;
                 float* dst = lane_sums + (uint64_t)gid * srs;
-#ifdef R3DG_EXP_ATOMSTORE  // timing experiment only (results invalid): plain stores for the atomics
-#define R3DG_FLUSH_ADD(p, v) (*(p) = (v))
-#elif defined(R3DG_EXP_NOSTORE)  // timing experiment only (results invalid): the epilogue without its stores
-#define R3DG_FLUSH_ADD(p, v) do { if ((v) == 1.2345e-30f) *(p) = 0.f; } while (0)
-#else
-#define R3DG_FLUSH_ADD(p, v) atomicAdd((p), (v))
-#endif
 #pragma unroll
                 for (int xb = 0; xb < NXB; ++xb)
                     if (ok && xb * 16 + nch < 4 + S) R3DG_FLUSH_ADD(dst + xb * 16, accX[xb][i]);
