@@ -423,7 +423,7 @@ __global__ void __launch_bounds__(kBlock) intermediate_glds_kernel(IntermediateA
             const float2 xy1 = *reinterpret_cast<const float2*>(st + NB + u1);
             const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
             const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
-            const f32x2 G = r3dg_expf2(pw0, pw1);
+            const f32x2 G = {r3dg_expf(pw0), r3dg_expf(pw1)};  // scalar chains, as the default blend
             step(j0, true, pw0, G.x);
             step(j1, has1, pw1, G.y);
         }
