@@ -33,11 +33,11 @@ HIP_FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall", "-W
 # render_bwd: the SLP vectorizer pairs the two unrolled blend steps into packed f32 ops plus
 # register shuffles (more instructions, 30 more VGPRs); plain scalar code measures faster; in
 # render_fwd it packs the blend's channel sums into v_pk_fma_f32 (4 cycles each, as two v_fma_f32):
-# scalar FMAs measured 1.5 % faster
+# scalar FMAs measured 1.5 % faster; brdf.hip: the BRDF forwards 1.5-2 % faster unpacked
 # brdf.hip: the render equation restates the oracle's operation sequence (no a*b+c contraction), so
 # the BRDF outputs are bit-identical to it
 PER_FILE_FLAGS = {"preprocess.hip": ["-ffp-contract=off"], "bvh.hip": ["-ffp-contract=off"],
-                  "brdf.hip": ["-ffp-contract=off"], "render_bwd.hip": ["-fno-slp-vectorize"],
+                  "brdf.hip": ["-ffp-contract=off", "-fno-slp-vectorize"], "render_bwd.hip": ["-fno-slp-vectorize"],
                   "render_fwd.hip": ["-fno-slp-vectorize"]}
 
 
