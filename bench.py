@@ -12,8 +12,9 @@ renders its own camera of the same scene (weak scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Rank 0 prints one JSON line. `roofline` prices renderCUDA fwd + bwd -- render_fwd_glds_kernel,
-render_bwd_glds_kernel and row_sum_kernel (the backward's per-instance reduction) -- with SURVEY.md
+Rank 0 prints one JSON line. `roofline` prices renderCUDA fwd + bwd -- render_fwd_glds_kernel and
+render_bwd_glds_kernel with its atomic second stage (plus the sums' memset; row_sum_kernel instead
+under R3DG_BWD_REDUCE=rows) -- with SURVEY.md
 §8d's algorithmic bytes exactly (272*L + 156*H*W + 16*tiles at S=11; the 12*L the forward also moves
 for its fused per-tile depth sort is reported apart, as `extra_bytes`) over their device time, from HIP
 events recorded inside each launch's dispatch on the launch stream during K further steps (the
@@ -104,6 +105,17 @@ def valu_roofline(v: dict | None, launch_ms: dict) -> dict | None:
         out["achieved"] = tot_i / tot_t
         out["frac"] = round(tot_i / tot_t / VALU_PEAK, 4)
     return out
+
+
+def binding(hbm_frac: float, valu: dict | None) -> str:
+    """What binds the blend, from the measured fractions of the two peaks: the larger one when it
+    exceeds 0.6, otherwise neither is saturated and the loop waits on latency (dependent LDS / exp
+    chains, the batch barrier)."""
+    vf = float(valu.get("frac", 0.0)) if valu else 0.0
+    top, name = max((hbm_frac, "hbm"), (vf, "valu"))
+    if top >= 0.6:
+        return name
+    return f"latency (hbm {hbm_frac:.2f}, valu {vf:.2f} of peak)"
 
 
 def cpu_baseline(scene) -> dict:
@@ -239,24 +251,33 @@ def bvh_visibility(means3D, scales, rots, dev) -> dict:
     return res
 
 
-def comm_probe(P: int, dev, world: int, backend: str, iters: int = 5) -> dict:
-    """The exchange's two collectives alone, at this run's size, outside the timed loop (DESIGN.md
-    §6 cost model): the all-reduce of the 22 dense gradient floats per Gaussian (means3D 3, opacity
-    1, scales 3, rotations 4, features 11) and the all-gather of every view's 3-float SH colour
-    gradient. Mean over `iters` after one warmup, barrier-bracketed, max over ranks. Bus bandwidth
-    as nccl-tests defines it: all-reduce 2(N-1)/N * bytes / t, all-gather (N-1)/N * N * bytes / t."""
+def comm_probe(seq: list, dev, world: int, backend: str, iters: int = 5) -> dict:
+    """The exchange's collectives alone, outside the timed loop (DESIGN.md §6 cost model): the exact
+    sequence one step issued (view_parallel.LAST_COLLECTIVES: the camera-centre all-gather, then per
+    chunk the all-reduce of the chunk's packed dense rows -- 22 floats per Gaussian -- and the
+    all-gather of its 3-float SH colour gradients), replayed back to back on the current stream.
+    Mean over `iters` after one warmup, barrier-bracketed, max over ranks. Bus bandwidth as
+    nccl-tests defines it: all-reduce 2(N-1)/N * bytes / t, all-gather (N-1)/N * N * bytes / t."""
     import torch
     import torch.distributed as dist
 
-    dense = torch.ones(P * 22, device=dev)
-    col = torch.ones(P, 3, device=dev)
-    buf = torch.empty(world, P, 3, device=dev)
-
-    def gather():
-        if backend == "nccl":
-            dist.all_gather_into_tensor(buf, col)
+    bufs = []
+    for kind, n in seq:
+        if kind == "all_reduce":
+            bufs.append((kind, torch.ones(n, device=dev), None))
         else:
-            dist.all_gather(list(buf.unbind(0)), col)
+            bufs.append((kind, torch.ones(n, device=dev), torch.empty(world, n, device=dev)))
+
+    def replay(only=None):
+        for kind, x, out in bufs:
+            if only and kind != only:
+                continue
+            if kind == "all_reduce":
+                dist.all_reduce(x)
+            elif backend == "nccl":
+                dist.all_gather_into_tensor(out, x)
+            else:
+                dist.all_gather(list(out.unbind(0)), x)
 
     def timed(fn):
         fn()
@@ -270,14 +291,20 @@ def comm_probe(P: int, dev, world: int, backend: str, iters: int = 5) -> dict:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    t_ar = timed(lambda: dist.all_reduce(dense))
-    t_ag = timed(gather)
-    ar_bytes, ag_bytes = dense.numel() * 4, col.numel() * 4
-    return {"backend": backend, "gaussians": P,
-            "all_reduce_dense22": {"bytes": ar_bytes, "ms": round(t_ar * 1e3, 4),
-                                   "bus_GBps": round(2 * (world - 1) / world * ar_bytes / t_ar / 1e9, 2)},
-            "all_gather_color3": {"bytes_per_rank": ag_bytes, "ms": round(t_ag * 1e3, 4),
-                                  "bus_GBps": round((world - 1) * ag_bytes / t_ag / 1e9, 2)}}
+    t_all = timed(replay)
+    t_ar = timed(lambda: replay("all_reduce"))
+    t_ag = timed(lambda: replay("all_gather"))
+    ar_bytes = 4 * sum(n for k, n in seq if k == "all_reduce")
+    ag_bytes = 4 * sum(n for k, n in seq if k == "all_gather")
+    return {"backend": backend, "collectives_per_step": len(seq),
+            "sequence": [[k, n] for k, n in seq],
+            "replay_ms": round(t_all * 1e3, 4),
+            "all_reduce": {"calls": sum(1 for k, _ in seq if k == "all_reduce"), "bytes": ar_bytes,
+                           "ms": round(t_ar * 1e3, 4),
+                           "bus_GBps": round(2 * (world - 1) / world * ar_bytes / t_ar / 1e9, 2) if t_ar else None},
+            "all_gather": {"calls": sum(1 for k, _ in seq if k == "all_gather"), "bytes_per_rank": ag_bytes,
+                           "ms": round(t_ag * 1e3, 4),
+                           "bus_GBps": round((world - 1) * ag_bytes / t_ag / 1e9, 2) if t_ag else None}}
 
 
 def main() -> None:
@@ -368,7 +395,7 @@ def main() -> None:
         tc = torch.tensor([t_comp], dtype=torch.float64, device=dev)
         dist.all_reduce(tc, op=dist.ReduceOp.MAX)
         t_comp = float(tc.item())
-        exchange = comm_probe(args.P, dev, world, backend)
+        exchange = comm_probe(list(view_parallel.LAST_COLLECTIVES["sequence"]), dev, world, backend)
     # per-kernel device times: K more steps with HIP events inside the profiled launches (kept out
     # of the timed region above)
     _C.profile_enable(args.steps + 1)
@@ -394,9 +421,11 @@ def main() -> None:
     # per-step device time of each stage
     avg = {k: v[1] / args.steps for k, v in prof.items()}
     launch = {k: (v[1] / v[0] if v[0] else 0.0) for k, v in prof.items()}
-    # renderCUDA fwd + bwd: the backward blend AND its per-instance reduction (row_sum_kernel sums
-    # the partial rows the reference accumulates with atomics, backward.cu:552-611)
-    # (with the atomic flush, R3DG_BWD_REDUCE=atomic, the row_sum slot times the sums' zeroing)
+    # renderCUDA fwd + bwd: the backward blend AND its per-instance reduction's second stage (the
+    # default atomic flush: the slot times the zeroing of the per-Gaussian sums; R3DG_BWD_REDUCE=rows:
+    # row_sum_kernel, which sums the partial rows the reference accumulates with atomics,
+    # backward.cu:552-611)
+    reduce_mode = "rows" if os.environ.get("R3DG_BWD_REDUCE", "").startswith("r") else "atomic"
     t_kern = (launch["render_fwd"] + launch["render_bwd"] + launch["row_sum"]) / 1e3
     achieved = (bf + bb) / t_kern / 1e9
     traffic = None
@@ -420,13 +449,14 @@ def main() -> None:
         "config": {"workload": "M1: rasterize_gaussians + rasterize_gaussians_backward, 1M Gaussians, 1920x1080, "
                                "S=11 features, SH degree 3, default shaders, pseudo normal",
                    "gaussians": args.P, "width": W, "height": H, "features": S_M1, "num_rendered": int(L),
-                   "parallelism": f"view-parallel dp{world} (per Gaussian: RCCL all-reduce of 22 floats + "
+                   "parallelism": f"view-parallel dp{world} (per Gaussian: RCCL all-reduce of the 22 packed dense floats + "
                                   f"all-gather of the 3-float SH colour gradient, SH sum rebuilt per rank; "
-                                  f"{args.chunks} chunks overlapped with the gather phase)"},
+                                  f"{args.chunks} chunks overlapped with the gather phase, 2 collectives per chunk "
+                                  f"+ 1 camera-centre all-gather per step)"},
         "views_per_s": round(world * args.steps / elapsed, 3),
-        # the blend kernels are bound by neither HBM (frac ~0.16) nor VALU issue (valu.frac ~0.5):
-        # by dependent LDS / exp latency and the batch barrier (DESIGN.md §4 "Can 0.40 be reached")
-        "roofline": {"bound": "latency", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        # priced against HBM (north_star: no dense contraction, the blend's bytes over 8 TB/s); which
+        # resource binds is derived from the measured fractions (DESIGN.md §4 "Can 0.40 be reached")
+        "roofline": {"bound": "hbm", "binding": binding(achieved / HBM_PEAK_GBS, valu), "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "renderCUDA fwd + bwd: render_fwd_glds_kernel + render_bwd_glds_kernel + the reduction's "
                                "second stage (the sums memset with the default atomic flush; row_sum_kernel with "
@@ -434,9 +464,14 @@ def main() -> None:
                      "algorithmic_bytes": bf + bb, "extra_bytes": fused_sort_bytes(L),
                      "extra_bytes_note": "fused per-tile depth sort in the forward (12 B per instance), not in frac",
                      "kernel_ms": round(t_kern * 1e3, 4), "valu": valu},
-        "kernel_ms": {k: round(v, 4) for k, v in avg.items() if prof[k][0]},
+        "kernel_ms": {("bwd_reduce_" + reduce_mode if k == "row_sum" else k): round(v, 4) for k, v in avg.items()
+                      if prof[k][0]},
+        "bwd_reduce": {"mode": reduce_mode,
+                       "stage": "hipMemsetAsync of the per-Gaussian sums (atomic flush inside render_bwd)"
+                       if reduce_mode == "atomic" else "row_sum_kernel over the partial rows"},
     }
     if exchange is not None:
+        res["collectives_per_step"] = exchange["collectives_per_step"]
         ms_comp = t_comp / args.steps * 1e3
         exchange["compute_only_ms_per_step"] = round(ms_comp, 4)
         exchange["exposed_exchange_ms_per_step"] = round(ms_step - ms_comp, 4)

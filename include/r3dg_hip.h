@@ -176,6 +176,14 @@ typedef struct r3dg_backward_outputs {
     int n_chunks;
     void (*chunk_done)(void* ctx, int chunk, int g_begin, int g_end);
     void* chunk_ctx;
+    /* Optional packed layout of the dense per-Gaussian gradients (0: dL_dmeans3D [P,3],
+     * dL_dopacity [P,1], dL_dscales [P,3], dL_drotations [P,4], dL_dfeatures [P,S] as above). A
+     * value >= 11 + S is the row stride, in floats, of all five: the caller points them at the
+     * columns 0, 3, 4, 7 and 11 of one [P, dense_stride] array, so a Gaussian range of the five is
+     * one contiguous span -- one collective per chunk for the view-parallel exchange
+     * (relightable3dgaussian_amd/view_parallel.py). Appended in round 5; zero-initialised callers
+     * keep the round-4 layout. */
+    int dense_stride;
 } r3dg_backward_outputs;
 
 /* RasterizeGaussiansBackwardCUDA (rasterize_points.cu:183-275). Every output element is written

@@ -326,6 +326,9 @@ __device__ __forceinline__ float fast_expf(float x) {
 // away from a 4e-6 band the decision equals the exact one; inside the band the step re-evaluates
 // with r3dg_expf (rare; one wave-uniform branch). Returns the exact-decision G.
 __device__ __forceinline__ float settle_threshold(float power, float opacity, float G) {
+#ifdef R3DG_HWEXP
+    return G;
+#endif
     const bool near = fabsf(__builtin_fmaf(opacity * G, 255.0f, -1.0f)) < 4e-6f;
 #ifndef R3DG_NOSETTLE
     if (__builtin_expect(__ballot(near) != 0ull, 0)) {
@@ -337,8 +340,24 @@ __device__ __forceinline__ float settle_threshold(float power, float opacity, fl
     return G;
 }
 
+// The blend's G = exp(power) in the forward kernels. Default: the shared bit-reproducible
+// r3dg_expf (n_contrib / final_T bit-exact against the oracle). R3DG_HWEXP (experiment build,
+// DESIGN.md §4): the hardware v_exp_f32 on power * log2(e) -- the backward's fast_expf, so forward
+// and backward take identical alpha decisions without the backward's settle step, but the bits are
+// not the oracle's (v_exp_f32 is not correctly rounded: tools/probe/vexp_cr.hip).
+__device__ __forceinline__ float blend_expf(float x) {
+#ifdef R3DG_HWEXP
+    return fast_expf(x);
+#else
+    return r3dg_expf(x);
+#endif
+}
+
 // settle_threshold for a pair of steps with one wave-uniform branch.
 __device__ __forceinline__ void settle_threshold2(float pw0, float o0, float& G0, float pw1, float o1, float& G1) {
+#ifdef R3DG_HWEXP
+    return;  // the forward used the same fast_expf: its decisions are these
+#endif
     const bool n0 = fabsf(__builtin_fmaf(o0 * G0, 255.0f, -1.0f)) < 4e-6f;
     const bool n1 = fabsf(__builtin_fmaf(o1 * G1, 255.0f, -1.0f)) < 4e-6f;
     if (__builtin_expect(__ballot(n0 || n1) != 0ull, 0)) {

@@ -176,6 +176,9 @@ struct GatherBwdArgs {
     float* dL_dsh;
     float* dL_dscales;
     float* dL_drotations;
+    // row strides (floats) of dL_dmeans3D / dL_dopacity / dL_dscales / dL_drotations / dL_dfeatures:
+    // 3, 1, 3, 4, S, or one packed [P, 11 + S] row each (r3dg_backward_outputs.dense_stride)
+    int ld_m3, ld_op, ld_sc, ld_rot, ld_f;
 };
 
 struct XyzNormalArgs {

@@ -927,6 +927,13 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     ga.dL_dsh = (s->M > 0) ? out->dL_dsh : nullptr;
     ga.dL_dscales = out->dL_dscales;
     ga.dL_drotations = out->dL_drotations;
+    R3DG_REQUIRE(out->dense_stride == 0 || out->dense_stride >= 11 + S,
+                 "rasterize_gaussians_backward: dense_stride must be 0 or >= 11 + S");
+    if (out->dense_stride > 0) {
+        ga.ld_m3 = ga.ld_op = ga.ld_sc = ga.ld_rot = ga.ld_f = out->dense_stride;
+    } else {
+        ga.ld_m3 = 3; ga.ld_op = 1; ga.ld_sc = 3; ga.ld_rot = 4; ga.ld_f = S;
+    }
     if (!g->sh) ga.sh = nullptr;
     // per-Gaussian phase over n_chunks 256-aligned ranges; chunk_done after each range's launch
     const int nchunks = std::max(1, std::min(out->n_chunks, (P + 255) / 256));

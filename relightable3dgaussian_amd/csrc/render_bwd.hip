@@ -5,20 +5,24 @@
 //
 // MI355X design (replaces the reference's per-pixel float atomicAdd scatter, ~(10+S) atomics
 // per contributing pixel, backward.cu:552-611):
-//   1. render_bwd_mfma_kernel: one workgroup per tile (longest tiles first) replays the tile's
-//      list back to front; wave w owns the tile's 8x8 quadrant w. Per live (instance, wave) pair
-//      a predicated blend step yields two per-pixel scalars w = alpha*T and q = G*dL/dalpha; the
-//      wave's 64-pixel reductions of 16 instances are two MFMA products (w x [colour, feature,
-//      depth grads], q x pixel moments) whose results go straight from the accumulators to one
-//      partial row per (instance, quadrant) at index 4 * slot + quadrant, flagged -- no
-//      cross-wave reduction, no per-chunk barriers. render_bwd_dpp_kernel is the DPP-reduction
-//      cross-check (R3DG_BWD=dpp) writing the same rows.
+//   1. render_bwd_glds_kernel: one workgroup per tile (longest tiles first) replays the forward's
+//      per-quadrant contribution lists back to front, the render records LDS-DMA-staged one batch
+//      ahead; wave w owns the tile's 8x8 quadrant w. Per visited (instance, wave) pair a predicated
+//      blend step yields two per-pixel scalars w = alpha*T and q = G*dL/dalpha; a wave's 64-pixel
+//      reductions of 13 instances are bf16-split MFMA products (w x [colour, feature, depth grads],
+//      q x pixel moments about the quadrant centre). Default (ATOM): each (instance, wave) row is
+//      expanded about the Gaussian's mean in the lanes and added into the per-Gaussian sums
+//      [P, SRS] with no-return f32 atomics -- the reference's accumulation at 1/64 of its atomics;
+//      the last bits depend on the atomics' arrival order, as the reference's do. w is split into
+//      two bf16 terms (|w - h - m| <= 2^-16 |w|), q into three (exact).
+//      R3DG_BWD_REDUCE=rows (!ATOM): one partial row per (instance, quadrant) at 4 * slot +
+//      quadrant, flagged, summed by
 //   2. row_sum_kernel: one 8-lane group per Gaussian sums its flagged partial rows (contiguous:
 //      slots are Gaussian-major, duplicateWithKeys order) in a fixed order and expands the
-//      quadrant-centred moments into the mean2D / conic / opacity gradients.
-//   3. gather_bwd_kernel: one thread per Gaussian runs the cov2D / projection / SH / cov3D
-//      backward. No global atomics anywhere: gradients are bitwise reproducible run to run (the
-//      reference's are not).
+//      quadrant-centred moments -- bitwise reproducible run to run.
+//      render_bwd_dpp_kernel (R3DG_BWD=dpp) is the DPP-reduction cross-check writing the same rows.
+//   3. gather_bwd_kernel: one thread per Gaussian expands the sums into the mean2D / conic / opacity
+//      gradients and runs the cov2D / projection / SH / cov3D backward.
 #include "r3dg_common.h"
 #include "r3dg_kernels.h"
 
@@ -258,29 +262,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // write address is the lane base plus a wave-uniform row offset.
 constexpr int WQS = 66;
 
-// lane `lane` (wave-uniform) of v takes the wave-uniform value x (v_cmp + v_cndmask)
-__device__ __forceinline__ int write_lane(int v, int x, int lane) {
-    return (int)(threadIdx.x & 63) == lane ? x : v;
-}
-
-// Lane that holds MFMA-group row r's bookkeeping (its partial row / Gaussian, mean offset): lane
-// i = r & 3 of 16-lane row r >> 2. The flush's lane group g (lanes 16g..16g+15) handles D row
-// 4g + i of accumulator element i, so row_bcast(v, i) -- DPP row_newbcast:i, one VALU, no LDS --
-// hands every lane of the group its row's value.
-__device__ __forceinline__ int row_lane(int r) { return 16 * (r >> 2) + (r & 3); }
-__device__ __forceinline__ int row_bcast(int v, int i) {
-    switch (i) {  // the DPP control must be an immediate (i is a constant after unrolling)
-        // (every lane reads a valid source lane: bound_ctrl, no `old` operand to materialise)
-        case 0: return __builtin_amdgcn_mov_dpp(v, 0x150, 0xf, 0xf, true);
-        case 1: return __builtin_amdgcn_mov_dpp(v, 0x151, 0xf, 0xf, true);
-        case 2: return __builtin_amdgcn_mov_dpp(v, 0x152, 0xf, 0xf, true);
-        default: return __builtin_amdgcn_mov_dpp(v, 0x153, 0xf, 0xf, true);
-    }
-}
-__device__ __forceinline__ float row_bcast(float v, int i) {
-    return __int_as_float(row_bcast(__float_as_int(v), i));
-}
-
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // Exact bf16 splits by truncation: h = the top 8 significant bits of x (its upper 16 bits), r = x - h
@@ -384,7 +365,10 @@ __device__ __forceinline__ void split_bf16x2(const float (&x)[8], bf16x8& h, bf1
 // [P, SRS] (the reference's own accumulation, backward.cu:552-611, at one atomic per channel per
 // (instance, wave) instead of per pixel): no partial rows, no row flags, no row_sum_kernel; sums
 // depend on the atomics' arrival order. !ATOM: the deterministic partial rows + row_sum_kernel.
-template <int SMAX, bool ATOM>
+// WS: bf16 terms of w in the X products (R3DG_BWD_SPLIT, default 2); WS = 1 is the one-term
+// reduction the gradient parity bar must reject (R3DG_BWD_WTERMS=1, tests/test_gpu_parity.py
+// test_one_term_reduction_fails_bar).
+template <int SMAX, bool ATOM, int WS = R3DG_BWD_SPLIT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SMAX <= 12 ? R3DG_BWD_WAVES : 1)))
 render_bwd_glds_kernel(RenderBwdArgs a) {
     constexpr int NB = R3DG_BWDG_NB;              // instances per batch (two batches staged)
@@ -462,13 +446,12 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
     }
     float u = 0.f;
     const float TFB = T_final * bg_dot;
-    int rowj = 0;  // group row r's partial-row index (4 * slot + quadrant) in lane row_lane(r) (ATOM: its Gaussian)
-    float d0xr = 0.f, d0yr = 0.f;  // ATOM: group row r's mean - quadrant centre in lane row_lane(r)
     const float qcx = (float)(tx * kTileX + (w & 1) * 8) + 3.5f, qcy = (float)(ty * kTileY + (w >> 1) * 8) + 3.5f;
     const int wmax = __builtin_amdgcn_readfirstlane(wave_max_int(last));
     const int max_last = block_max_last(wmax, s_max_last);
     const int RS = a.RS;
     const int nch = l & 15;
+    const bool lane0 = l == 0;
     const float4* st = stage;  // staging buffer of the current batch
 
     auto step = [&](int j, int p, bool live, float opacity, float power, float G, float& wv, float& qv,
@@ -545,33 +528,31 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) wv[i] = src[i];
             bf16x8 h, m, o;
-#if R3DG_BWD_SPLIT == 1  // timing experiment only (results inexact): one term, one product
-            split_bf16x2(wv, h, m);
-            (void)o;
-            (void)m;
+            if constexpr (WS == 1) {  // one term, one product (inexact: the negative parity test)
+                split_bf16x2(wv, h, m);
 #pragma unroll
-            for (int xb = 0; xb < NXB; ++xb)
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
-#elif R3DG_BWD_SPLIT == 2
-            split_bf16x2(wv, h, m);
-            (void)o;
+                for (int xb = 0; xb < NXB; ++xb)
+                    accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
+            } else if constexpr (WS == 2) {
+                split_bf16x2(wv, h, m);
 #pragma unroll
-            for (int xb = 0; xb < NXB; ++xb) {
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bXh[xb][b], accX[xb], 0, 0, 0);
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXl[xb][b], accX[xb], 0, 0, 0);
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
+                for (int xb = 0; xb < NXB; ++xb) {
+                    accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bXh[xb][b], accX[xb], 0, 0, 0);
+                    accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXl[xb][b], accX[xb], 0, 0, 0);
+                    accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
+                }
+            } else {
+                split_bf16x3(wv, h, m, o);
+#pragma unroll
+                for (int xb = 0; xb < NXB; ++xb) {
+                    accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o, bXh[xb][b], accX[xb], 0, 0, 0);
+                    accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bXl[xb][b], accX[xb], 0, 0, 0);
+                    accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bXh[xb][b], accX[xb], 0, 0, 0);
+                    accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXl[xb][b], accX[xb], 0, 0, 0);
+                    accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
+                }
             }
-#else
-            split_bf16x3(wv, h, m, o);
-#pragma unroll
-            for (int xb = 0; xb < NXB; ++xb) {
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o, bXh[xb][b], accX[xb], 0, 0, 0);
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bXl[xb][b], accX[xb], 0, 0, 0);
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bXh[xb][b], accX[xb], 0, 0, 0);
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXl[xb][b], accX[xb], 0, 0, 0);
-                accX[xb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bXh[xb][b], accX[xb], 0, 0, 0);
-            }
-#endif
+            (void)o;
         }
         // q rows times the moments on the bf16 MFMA (16 cycles per K = 32, against 32 per K = 4 in
         // f32): three exact-sum bf16 terms of q per K-block
@@ -599,42 +580,64 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             accY = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o, yb[b], accY, 0, 0, 0);
 #endif
         }
-#ifdef R3DG_EXP_NOEPI  // timing experiment only (results invalid): no broadcasts, expansion, stores
-        if (accX[0][0] == 1.2345e-30f && accY[0] == 1.2345e-30f) a.sums[l] = accX[0][1] + accY[1] + accX[0][2] + accY[2];
+        // Group row r's bookkeeping sits in the pad columns of its w|q image rows (written by lane 0
+        // at the visit): the instance's mean (x, y) at w row r, columns 64-65, and its Gaussian
+        // (ATOM) or partial row (4 * slot + quadrant) at q row r, column 64. Lane group g handles
+        // D rows 4g + i of accumulator element i: one broadcast LDS read per row and value.
+        uint32_t rid[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            rid[i] = reinterpret_cast<const uint32_t*>(wq)[(GRP + (l >> 4) * 4 + i) * WQS + 64];
+#ifdef R3DG_EXP_NOEPI  // timing experiment only (results invalid): no expansion, no stores
+        if (accX[0][0] == 1.2345e-30f && accY[0] == 1.2345e-30f) a.sums[l] = accX[0][1] + accY[1] + rid[0];
         wave_lds_sync();
         return;
 #endif
         if constexpr (ATOM) {
+            // The moments about the quadrant centre, expanded about the Gaussian's mean once per
+            // row (expand_moments, as row_sum_kernel): D rows go through a 16 x 8 LDS tile in w rows
+            // 0-1 (free once the MFMA operands were read), lane rr = l & 15 expands row rr and writes
+            // it back, then every lane adds its (row, moment) element as before.
+            float* const yt = wq;
+            auto yoff = [](int row) { return (row >> 3) * WQS + (row & 7) * 8; };
+            if (nch < 6) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) yt[yoff((l >> 4) * 4 + i) + nch] = accY[i];
+            }
+            wave_lds_sync();
+            {
+                const int rr = l & 15;
+                const float2* yr = reinterpret_cast<const float2*>(yt + yoff(rr));
+                const float2 m01 = yr[0], m23 = yr[1], m45 = yr[2];
+                const float2 mxy = *reinterpret_cast<const float2*>(wq + rr * WQS + 64);
+                const float sm[6] = {m01.x, m01.y, m23.x, m23.y, m45.x, m45.y};
+                float e[6];
+                expand_moments(sm, mxy.x - qcx, mxy.y - qcy, e);
+                if (l < 16) {
+                    float2* yw = reinterpret_cast<float2*>(yt + yoff(rr));
+                    yw[0] = make_float2(e[0], e[1]);
+                    yw[1] = make_float2(e[2], e[3]);
+                    yw[2] = make_float2(e[4], e[5]);
+                }
+            }
+            wave_lds_sync();
+            // the four expanded elements of this lane, read together (the compiler would otherwise
+            // sink each read into its atomic's masked branch: four dependent LDS round trips)
+            float ev[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ev[i] = yt[yoff((l >> 4) * 4 + i) + (nch < 6 ? nch : 0)];
+            asm volatile("" ::"v"(ev[0]), "v"(ev[1]), "v"(ev[2]), "v"(ev[3]));
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int row = (l >> 4) * 4 + i;
-                const uint32_t gid = (uint32_t)row_bcast(rowj, i);
-                const float d0x = row_bcast(d0xr, i), d0y = row_bcast(d0yr, i);
-                // the row's moments about the quadrant centre, S0 / Sx / Sy from lanes 0..2 of the row
-                const float s0 = row_bcast(accY[i], 0), s1 = row_bcast(accY[i], 1), s2 = row_bcast(accY[i], 2);
-                // computed by every lane, stored under one lane mask per atomic (no branch around
-                // the expansion); the address is one u32 x u32 product per row. (Adding 0 from the
-                // masked lanes instead measured 23x slower: rows past the group, never written,
-                // all name Gaussian 0, and every wave's zeros contend on its row.)
+                // (only the two atomics under lane masks; adding 0 from the masked lanes instead
+                // measured 23x slower: rows past the group all name one Gaussian and contend)
                 const bool ok = row < r;
-                float* dst = lane_sums + (uint64_t)gid * srs;
+                float* dst = lane_sums + (uint64_t)rid[i] * srs;
 #pragma unroll
                 for (int xb = 0; xb < NXB; ++xb)
                     if (ok && xb * 16 + nch < 4 + S) R3DG_FLUSH_ADD(dst + xb * 16, accX[xb][i]);
-                // expand_moments, one output per lane (the same operations as row_sum_kernel's)
-                // (every candidate computed and selected: the lanes of a row take all six branches)
-                const float sk = accY[i];
-                const float e1 = d0x * s0 - s1, e2 = d0y * s0 - s2;
-                const float e3 = d0x * d0x * s0 - 2.f * d0x * s1 + sk;
-                const float e4 = d0x * d0y * s0 - d0x * s2 - d0y * s1 + sk;
-                const float e5 = d0y * d0y * s0 - 2.f * d0y * s2 + sk;
-                float e = s0;
-                e = nch == 1 ? e1 : e;
-                e = nch == 2 ? e2 : e;
-                e = nch == 3 ? e3 : e;
-                e = nch == 4 ? e4 : e;
-                e = nch == 5 ? e5 : e;
-                if (ok && nch < 6) R3DG_FLUSH_ADD(dst + XW, e);
+                if (ok && nch < 6) R3DG_FLUSH_ADD(dst + XW, ev[i]);
             }
             wave_lds_sync();
             return;
@@ -642,7 +645,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = (l >> 4) * 4 + i;
-            const uint32_t base = (uint32_t)row_bcast(rowj, i);
+            const uint32_t base = rid[i];
             if (row < r) {
                 // 32-bit offset in float4 units (RS is a multiple of 8 floats): 4L rows x RS / 4
                 // stay below 2^32 (checked on the host: L * RS < 2^32, L < 178M at S <= 12)
@@ -766,25 +769,26 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             (void)ok0;
             (void)ok1;
 #endif
-            // every visited instance was blended by a pixel of this wave: one group row each
+            // every visited instance was blended by a pixel of this wave: one group row each; lane 0
+            // also writes the row's bookkeeping into the image rows' pad columns (the flush reads it)
             {
                 float* wr = wq + r * WQS + l;
                 wr[0] = wv0;
                 wr[GRP * WQS] = qv0;
-                rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j0), row_lane(r));
-                if constexpr (ATOM) {
-                    d0xr = l == row_lane(r) ? xy0.x - qcx : d0xr;
-                    d0yr = l == row_lane(r) ? xy0.y - qcy : d0yr;
+                const uint32_t id0 = __builtin_amdgcn_readlane(row_l, j0);
+                if (lane0) {
+                    *reinterpret_cast<float2*>(wq + r * WQS + 64) = xy0;
+                    reinterpret_cast<uint32_t*>(wq)[(GRP + r) * WQS + 64] = id0;
                 }
             }
             if (has1) {
                 float* wr = wq + (r + 1) * WQS + l;
                 wr[0] = wv1;
                 wr[GRP * WQS] = qv1;
-                rowj = write_lane(rowj, (int)__builtin_amdgcn_readlane(row_l, j1), row_lane(r + 1));
-                if constexpr (ATOM) {
-                    d0xr = l == row_lane(r + 1) ? xy1.x - qcx : d0xr;
-                    d0yr = l == row_lane(r + 1) ? xy1.y - qcy : d0yr;
+                const uint32_t id1 = __builtin_amdgcn_readlane(row_l, j1);
+                if (lane0) {
+                    *reinterpret_cast<float2*>(wq + (r + 1) * WQS + 64) = xy1;
+                    reinterpret_cast<uint32_t*>(wq)[(GRP + r + 1) * WQS + 64] = id1;
                 }
             }
             r += has1 ? 2 : 1;
@@ -829,8 +833,19 @@ static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
     // DMA-staged MFMA kernel. Both write the same partial rows (the forward's contribution set).
     const char* e = getenv("R3DG_BWD");  // read per launch: tests switch it at run time
     const bool dpp = e && e[0] == 'd';
+    // R3DG_BWD_WTERMS=1 / 3 (S in 9..12, atomic sums only; refused otherwise): w in one bf16 term,
+    // the inexact reduction the gradient parity bar must reject, or in three (exact products), the
+    // reference point of the default two-term split's error (tests/test_gpu_parity.py)
+    const char* wt = getenv("R3DG_BWD_WTERMS");
+    const int wterms = wt && wt[0] ? wt[0] - '0' : 0;
     const int grid = padded_tile_grid(a.num_tiles);
-    if (dpp)
+    if (wterms) {
+        if (SMAX != 12 || !a.sums_atomic || dpp || (wterms != 1 && wterms != 3)) return hipErrorInvalidValue;
+        if (wterms == 1)
+            launch_kernel(render_bwd_glds_kernel<SMAX, true, 1>, dim3(grid), dim3(kBlock), stream, a);
+        else
+            launch_kernel(render_bwd_glds_kernel<SMAX, true, 3>, dim3(grid), dim3(kBlock), stream, a);
+    } else if (dpp)
         launch_kernel(render_bwd_dpp_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
     else if (a.sums_atomic)
         launch_kernel(render_bwd_glds_kernel<SMAX, true>, dim3(grid), dim3(kBlock), stream, a);
@@ -969,22 +984,22 @@ __device__ __forceinline__ void gather_gaussian(const GatherBwdArgs& a, int g, c
     a.dL_dmeans2D[3 * g + 0] = s[kRowMean + 0];
     a.dL_dmeans2D[3 * g + 1] = s[kRowMean + 1];
     a.dL_dmeans2D[3 * g + 2] = s[kRowMean + 2];
-    a.dL_dopacity[g] = s[kRowOpacity];
+    a.dL_dopacity[(size_t)g * a.ld_op] = s[kRowOpacity];
     a.dL_dcolors[3 * g + 0] = s[kRowColor + 0];
     a.dL_dcolors[3 * g + 1] = s[kRowColor + 1];
     a.dL_dcolors[3 * g + 2] = s[kRowColor + 2];
 #pragma unroll
     for (int c = 0; c < SMAX; ++c)
-        if (c < a.S) a.dL_dfeatures[(size_t)g * a.S + c] = s[kRowFeat + c];
+        if (c < a.S) a.dL_dfeatures[(size_t)g * a.ld_f + c] = s[kRowFeat + c];
 
-    float* dmean3 = a.dL_dmeans3D + 3 * g;
+    float* dmean3 = a.dL_dmeans3D + (size_t)g * a.ld_m3;
     float* dcov = a.dL_dcov3D + 6 * g;
     if (!(a.radii[g] > 0)) {
         dmean3[0] = dmean3[1] = dmean3[2] = 0.f;
         for (int i = 0; i < 6; ++i) dcov[i] = 0.f;
         for (int i = 0; i < 3 * a.M; ++i) shl[i] = 0.f;
-        for (int i = 0; i < 3; ++i) a.dL_dscales[3 * g + i] = 0.f;
-        for (int i = 0; i < 4; ++i) a.dL_drotations[4 * g + i] = 0.f;
+        for (int i = 0; i < 3; ++i) a.dL_dscales[(size_t)g * a.ld_sc + i] = 0.f;
+        for (int i = 0; i < 4; ++i) a.dL_drotations[(size_t)g * a.ld_rot + i] = 0.f;
         return;
     }
 
@@ -1080,10 +1095,11 @@ __device__ __forceinline__ void gather_gaussian(const GatherBwdArgs& a, int g, c
         const float3 sc = make_float3(a.scales[3 * g], a.scales[3 * g + 1], a.scales[3 * g + 2]);
         const float4 q = make_float4(a.rotations[4 * g], a.rotations[4 * g + 1], a.rotations[4 * g + 2],
                                      a.rotations[4 * g + 3]);
-        cov3d_backward(sc, a.scale_modifier, q, dcov, a.dL_dscales + 3 * g, a.dL_drotations + 4 * g);
+        cov3d_backward(sc, a.scale_modifier, q, dcov, a.dL_dscales + (size_t)g * a.ld_sc,
+                       a.dL_drotations + (size_t)g * a.ld_rot);
     } else {
-        for (int i = 0; i < 3; ++i) a.dL_dscales[3 * g + i] = 0.f;
-        for (int i = 0; i < 4; ++i) a.dL_drotations[4 * g + i] = 0.f;
+        for (int i = 0; i < 3; ++i) a.dL_dscales[(size_t)g * a.ld_sc + i] = 0.f;
+        for (int i = 0; i < 4; ++i) a.dL_drotations[(size_t)g * a.ld_rot + i] = 0.f;
     }
 }
 

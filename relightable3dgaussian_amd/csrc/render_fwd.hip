@@ -260,7 +260,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
                 // two scalar exp chains, interleaved by the scheduler (the packed pair, r3dg_expf2,
                 // needs an s_nop between its dependent v_pk_fma_f32: 0.3 % slower at M1)
-                const f32x2 G = {r3dg_expf(pw0), r3dg_expf(pw1)};
+                const f32x2 G = {blend_expf(pw0), blend_expf(pw1)};
                 step(j0, true, co0.w, pw0, G.x);
                 step(j1, has1, co1.w, pw1, G.y);
                 if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
@@ -423,7 +423,7 @@ __global__ void __launch_bounds__(kBlock) intermediate_glds_kernel(IntermediateA
             const float2 xy1 = *reinterpret_cast<const float2*>(st + NB + u1);
             const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
             const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
-            const f32x2 G = {r3dg_expf(pw0), r3dg_expf(pw1)};  // scalar chains, as the default blend
+            const f32x2 G = {blend_expf(pw0), blend_expf(pw1)};  // scalar chains, as the default blend
             step(j0, true, pw0, G.x);
             step(j1, has1, pw1, G.y);
         }

@@ -150,22 +150,27 @@ BwdResult backward_impl(const torch::Tensor& background, const torch::Tensor& me
                         const torch::Tensor& geomBuffer, int64_t R, const torch::Tensor& binningBuffer,
                         const torch::Tensor& imageBuffer, bool backward_geometry, bool debug, int H, int W,
                         bool color_hwc, bool feature_native, int n_chunks = 1,
-                        const py::object& chunk_cb = py::none()) {
+                        const py::object& chunk_cb = py::none(), bool packed_dense = false) {
     const torch::Device dev = means3D.device();
     const c10::OptionalDeviceGuard guard(dev);
     const int P = (int)means3D.size(0);
     const int S = features.numel() == 0 && features.dim() < 2 ? 0 : (int)features.size(1);
     const int M = sh.numel() == 0 ? 0 : (int)sh.size(1);
     auto fopt = means3D.options().dtype(torch::kFloat32);
-    torch::Tensor dL_dmeans3D = torch::empty({P, 3}, fopt);
+    // packed_dense: the five dense gradients are column views of one [P, 11 + S] array (means3D 3,
+    // opacity 1, scales 3, rotations 4, features S), so a Gaussian range of them is one contiguous
+    // span (r3dg_backward_outputs.dense_stride; one collective per chunk in view_parallel.py)
+    const int DW = 11 + S;
+    torch::Tensor dense = packed_dense ? torch::empty({P, DW}, fopt) : torch::Tensor();
+    torch::Tensor dL_dmeans3D = packed_dense ? dense.narrow(1, 0, 3) : torch::empty({P, 3}, fopt);
     torch::Tensor dL_dmeans2D = torch::empty({P, 3}, fopt);
-    torch::Tensor dL_dfeatures = torch::empty({P, S}, fopt);
+    torch::Tensor dL_dfeatures = packed_dense ? dense.narrow(1, 11, S) : torch::empty({P, S}, fopt);
     torch::Tensor dL_dcolors = torch::empty({P, 3}, fopt);
-    torch::Tensor dL_dopacity = torch::empty({P, 1}, fopt);
+    torch::Tensor dL_dopacity = packed_dense ? dense.narrow(1, 3, 1) : torch::empty({P, 1}, fopt);
     torch::Tensor dL_dcov3D = torch::empty({P, 6}, fopt);
     torch::Tensor dL_dsh = torch::empty({P, M, 3}, fopt);
-    torch::Tensor dL_dscales = torch::empty({P, 3}, fopt);
-    torch::Tensor dL_drotations = torch::empty({P, 4}, fopt);
+    torch::Tensor dL_dscales = packed_dense ? dense.narrow(1, 4, 3) : torch::empty({P, 3}, fopt);
+    torch::Tensor dL_drotations = packed_dense ? dense.narrow(1, 7, 4) : torch::empty({P, 4}, fopt);
     if (P == 0) return {dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dfeatures, dL_dcov3D, dL_dsh,
                         dL_dscales, dL_drotations};
 
@@ -196,6 +201,7 @@ BwdResult backward_impl(const torch::Tensor& background, const torch::Tensor& me
     o.dL_dfeatures = S > 0 ? dL_dfeatures.data_ptr<float>() : nullptr; o.dL_dcov3D = dL_dcov3D.data_ptr<float>();
     o.dL_dsh = M > 0 ? dL_dsh.data_ptr<float>() : nullptr; o.dL_dscales = dL_dscales.data_ptr<float>();
     o.dL_drotations = dL_drotations.data_ptr<float>();
+    o.dense_stride = packed_dense ? DW : 0;
     // chunked delivery: the Python callable runs (GIL held: we are inside the pybind call) after
     // each Gaussian range's kernels are enqueued; an exception is re-raised after the C call
     struct ChunkCtx {
@@ -203,8 +209,10 @@ BwdResult backward_impl(const torch::Tensor& background, const torch::Tensor& me
         py::tuple outs;  // the 9 output tensors, handed to the callback
         bool failed = false;
         std::string what;
-    } cctx{&chunk_cb, py::make_tuple(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dfeatures, dL_dcov3D,
-                                     dL_dsh, dL_dscales, dL_drotations)};
+    } cctx{&chunk_cb, packed_dense ? py::make_tuple(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dfeatures,
+                                                    dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, dense)
+                                   : py::make_tuple(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dfeatures,
+                                                    dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)};
     o.n_chunks = n_chunks;
     if (!chunk_cb.is_none()) {
         o.chunk_ctx = &cctx;
@@ -287,6 +295,26 @@ BwdResult rasterize_gaussians_backward_chunked(
                          cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_opacity,
                          dL_dout_depth, dL_dout_feature, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
                          backward_geometry, debug, (int)H, (int)W, color_hwc, feature_native, (int)n_chunks, chunk_cb);
+}
+
+// rasterize_gaussians_backward_chunked with the dense gradients packed (packed_dense above): the
+// callback's outputs carry a 10th tensor, the [P, 11 + S] array whose rows [g_begin, g_end) hold
+// the chunk's means3D / opacity / scales / rotations / features gradients contiguously.
+BwdResult rasterize_gaussians_backward_chunked_packed(
+    const torch::Tensor& background, const torch::Tensor& means3D, const torch::Tensor& features,
+    const torch::Tensor& radii, const torch::Tensor& colors, const torch::Tensor& scales,
+    const torch::Tensor& rotations, double scale_modifier, const torch::Tensor& cov3D_precomp,
+    const torch::Tensor& viewmatrix, const torch::Tensor& projmatrix, double tan_fovx, double tan_fovy,
+    const torch::Tensor& dL_dout_color, const torch::Tensor& dL_dout_opacity, const torch::Tensor& dL_dout_depth,
+    const torch::Tensor& dL_dout_feature, const torch::Tensor& sh, int64_t degree, const torch::Tensor& campos,
+    const torch::Tensor& geomBuffer, int64_t R, const torch::Tensor& binningBuffer, const torch::Tensor& imageBuffer,
+    bool backward_geometry, bool debug, int64_t H, int64_t W, bool color_hwc, bool feature_native, int64_t n_chunks,
+    const py::object& chunk_cb) {
+    return backward_impl(background, means3D, features, radii, colors, scales, rotations, scale_modifier,
+                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_opacity,
+                         dL_dout_depth, dL_dout_feature, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                         backward_geometry, debug, (int)H, (int)W, color_hwc, feature_native, (int)n_chunks, chunk_cb,
+                         true);
 }
 
 // View-parallel SH-gradient exchange (include/r3dg_hip.h): this view's clamp-masked colour
@@ -870,6 +898,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     // extensions
     m.def("rasterize_gaussians_backward_ex", &rasterize_gaussians_backward_ex);
     m.def("rasterize_gaussians_backward_chunked", &rasterize_gaussians_backward_chunked);
+    m.def("rasterize_gaussians_backward_chunked_packed", &rasterize_gaussians_backward_chunked_packed);
     m.def("render_equation_forward_with_rand", &render_equation_forward_with_rand);
     m.def("rasterizer_state", &rasterizer_state);
     m.def("sh_color_grads", &sh_color_grads);

@@ -121,87 +121,127 @@ def _all_gather_into(buf, d, group=None):
     return dist.all_gather(list(buf.unbind(0)), d, group=group, async_op=True)
 
 
-def chunk_all_reduce_hook(works: list, group=None, stream=None):
-    """Chunk callback for `_C.rasterize_gaussians_backward_chunked`: all-reduces the exchanged
-    gradient slices of Gaussians [g0, g1) (rows of contiguous [P, ...] tensors, so each slice is
-    contiguous) on a communication stream that first waits for the chunk's kernels, while the
-    compute stream goes on with the next chunk. `works` collects the async handles."""
+# index of the packed [P, 11 + S] dense-gradient array in the chunk callback's outputs
+# (_C.rasterize_gaussians_backward_chunked_packed: means3D 3 | opacity 1 | scales 3 | rotations 4 |
+# features S per row, the DENSE_FIELDS in order)
+PACKED_INDEX = 9
+# collectives issued by the last backward_all_reduce call (bench.py reports it per step)
+LAST_COLLECTIVES = {"count": 0, "sequence": []}
+
+
+def _comm_stream(stream=None):
+    import torch
+
+    if stream is not None:
+        return stream
+    cur = torch.cuda.current_stream()
+    return _COMM.setdefault(cur.device, torch.cuda.Stream(device=cur.device))
+
+
+def _after_current(comm):
+    """The communication stream waits for what the compute stream has enqueued so far."""
+    import torch
+
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream())
+    comm.wait_event(ev)
+
+
+def chunk_all_reduce_hook(works: list, seq: list, group=None, stream=None):
+    """Chunk callback for `_C.rasterize_gaussians_backward_chunked_packed`: all-reduces the chunk's
+    rows of the packed dense array (one contiguous span) and of the SH block on a communication
+    stream that first waits for the chunk's kernels, while the compute stream goes on with the next
+    chunk. `works` collects the async handles, `seq` the (kind, floats) of each collective."""
     import torch
     import torch.distributed as dist
 
     def hook(chunk, g0, g1, outs):
-        cur = torch.cuda.current_stream()
-        comm = stream
-        if comm is None:
-            comm = _COMM.setdefault(cur.device, torch.cuda.Stream(device=cur.device))
-        ev = torch.cuda.Event()
-        ev.record(cur)
-        comm.wait_event(ev)
+        comm = _comm_stream(stream)
+        _after_current(comm)
         with torch.cuda.stream(comm):
-            for _, i in GRAD_FIELDS:
-                t = outs[i]
+            for t in (outs[PACKED_INDEX], outs[SH_INDEX]):
                 if t.numel():
                     works.append(dist.all_reduce(t[g0:g1], group=group, async_op=True))
+                    seq.append(("all_reduce", t[g0:g1].numel()))
 
     return hook
 
 
-def chunk_views_hook(_C, works: list, gathered: list, geom, P: int, group=None, stream=None):
-    """Chunk callback of the "views" exchange: the chunk's dense fields are all-reduced and its
-    clamp-masked colour gradients (r3dg_sh_color_grads, enqueued on the compute stream behind the
-    chunk's kernels) all-gathered into [N, n, 3], both on the communication stream."""
+def chunk_views_hook(_C, works: list, gathered: list, seq: list, geom, P: int, group=None, stream=None):
+    """Chunk callback of the "views" exchange: the chunk's rows of the packed dense array (22
+    floats per Gaussian at S = 11, one contiguous span) are all-reduced and its clamp-masked colour
+    gradients (r3dg_sh_color_grads, enqueued on the compute stream behind the chunk's kernels)
+    all-gathered into [N, n, 3], both on the communication stream: two collectives per chunk."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
 
     def hook(chunk, g0, g1, outs):
-        cur = torch.cuda.current_stream()
         sh_on = outs[SH_INDEX].numel() > 0
         d = _C.sh_color_grads(geom, P, outs[COLOR_INDEX], g0, g1) if sh_on else None
-        comm = stream
-        if comm is None:
-            comm = _COMM.setdefault(cur.device, torch.cuda.Stream(device=cur.device))
-        ev = torch.cuda.Event()
-        ev.record(cur)
-        comm.wait_event(ev)
+        comm = _comm_stream(stream)
+        _after_current(comm)
         with torch.cuda.stream(comm):
-            for _, i in DENSE_FIELDS:
-                t = outs[i]
-                if t.numel():
-                    works.append(dist.all_reduce(t[g0:g1], group=group, async_op=True))
+            dense = outs[PACKED_INDEX][g0:g1]
+            works.append(dist.all_reduce(dense, group=group, async_op=True))
+            seq.append(("all_reduce", dense.numel()))
             if sh_on:
                 buf = torch.empty((world, g1 - g0, 3), dtype=d.dtype, device=d.device)
                 works.append(_all_gather_into(buf, d, group))
+                seq.append(("all_gather", d.numel()))
                 gathered.append((g0, buf, d, len(works)))  # the chunk's exchange = works[:len]
 
     return hook
 
 
+def gather_campos_async(campos, group=None, stream=None):
+    """Start the all-gather of every rank's camera centre ([N, 3], rank order) on the
+    communication stream; returns (buffer, work) -- wait on the work before reading the buffer."""
+    import torch
+    import torch.distributed as dist
+
+    comm = _comm_stream(stream)
+    _after_current(comm)
+    c = campos.reshape(1, 3).contiguous()
+    with torch.cuda.stream(comm):
+        buf = torch.empty((dist.get_world_size(group), 1, 3), dtype=c.dtype, device=c.device)
+        work = _all_gather_into(buf, c, group)
+    return buf, work
+
+
 def backward_all_reduce(_C, bwd_args, n_chunks: int = 4, group=None, sh_exchange: str = "views"):
-    """rasterize_gaussians_backward_chunked(*bwd_args, n_chunks, hook) with the per-Gaussian
+    """rasterize_gaussians_backward_chunked_packed(*bwd_args, n_chunks, hook) with the per-Gaussian
     gradients summed over ranks chunk by chunk, overlapped with the remaining per-Gaussian kernels
     (the blend must finish before any Gaussian's gradient is final, so only that phase overlaps).
     `bwd_args` is the rasterize_gaussians_backward_ex argument list + (color_hwc, feature_native).
     sh_exchange "views" (default) all-gathers per-view colour gradients and rebuilds the SH sum
-    on every rank; "allreduce" all-reduces the SH block like the other fields.
-    Returns the backward 9-tuple; the current stream waits for the exchange."""
+    on every rank; "allreduce" all-reduces the SH block like the other fields. Per step: one
+    asynchronous all-gather of the camera centres ("views") + two collectives per chunk (9 at 4
+    chunks; LAST_COLLECTIVES records them). Returns the backward 9-tuple (the dense gradients are
+    column views of one packed array); the current stream waits for the exchange."""
     import torch
     import torch.distributed as dist
 
-    works, gathered = [], []
+    works, gathered, seq = [], [], []
     multi = dist.is_initialized() and dist.get_world_size(group) > 1
     if not multi:
+        LAST_COLLECTIVES.update(count=0, sequence=[])
         return _C.rasterize_gaussians_backward_chunked(*bwd_args, 1, None)
     if sh_exchange == "allreduce":
-        hook = chunk_all_reduce_hook(works, group)
+        hook = chunk_all_reduce_hook(works, seq, group)
     else:
         means3D, sh, degree, campos, geom = bwd_args[1], bwd_args[17], bwd_args[18], bwd_args[19], bwd_args[20]
-        cams = gather_campos(campos, group)
-        hook = chunk_views_hook(_C, works, gathered, geom, means3D.shape[0], group)
-    grads = _C.rasterize_gaussians_backward_chunked(*bwd_args, n_chunks, hook)
+        cams_buf, cams_work = gather_campos_async(campos, group)
+        seq.append(("all_gather", 3))
+        hook = chunk_views_hook(_C, works, gathered, seq, geom, means3D.shape[0], group)
+    grads = _C.rasterize_gaussians_backward_chunked_packed(*bwd_args, n_chunks, hook)
     cur = torch.cuda.current_stream()
     done = 0
+    if gathered:
+        cams_work.wait()
+        cams = cams_buf.reshape(-1, 3)
+        cams_buf.record_stream(cur)
     for g0, buf, _, upto in gathered:
         # every rank rebuilds the same SH gradient sum, chunk by chunk: a chunk's rebuild waits for
         # that chunk's collectives only and overlaps the later chunks' communication
@@ -212,6 +252,9 @@ def backward_all_reduce(_C, bwd_args, n_chunks: int = 4, group=None, sh_exchange
         buf.record_stream(cur)  # allocated on the communication stream, read here
     for w in works[done:]:
         w.wait()
+    if sh_exchange != "allreduce" and not gathered:
+        cams_work.wait()
+    LAST_COLLECTIVES.update(count=len(seq), sequence=seq)
     return grads
 
 

@@ -103,6 +103,52 @@ def assert_brdf(name, got, ref, summed=False):
         assert_close(name, got, ref, 1e-4, 0.0)
 
 
+# ------------------------------------------------------------------------------------------------
+# raster-gradient parity (HIP backward vs the oracle)
+# ------------------------------------------------------------------------------------------------
+def grad_stats(got, ref):
+    """(max |got - ref| / max |ref|, the largest elementwise relative error over the elements with
+    |ref| > 1e-3 max |ref|): the two numbers a gradient bar is set from."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    if ref.size == 0:
+        return 0.0, 0.0
+    d = np.abs(got - ref)
+    m = float(np.abs(ref).max())
+    if m == 0.0:
+        return float(d.max()), 0.0
+    big = np.abs(ref) > 1e-3 * m
+    rel = float((d[big] / np.abs(ref[big])).max()) if big.any() else 0.0
+    return float(d.max()) / m, rel
+
+
+def check_grad(tag, name, got, ref, rel, frac):
+    """Assert |got - ref| <= rel |ref| + frac max|ref| elementwise, after printing grad_stats (and
+    appending them to $R3DG_GRAD_REPORT as a JSON line, the measurement DESIGN.md §5 records)."""
+    import json
+    import os
+
+    f, r = grad_stats(got, ref)
+    print(f"grad {tag} {name}: max|d|/max|ref| {f:.2e}, max rel (|ref| > 1e-3 max) {r:.2e}")
+    path = os.environ.get("R3DG_GRAD_REPORT")
+    if path:
+        # the smallest frac that passes together with each rel (the bar's trade-off curve)
+        g64 = np.asarray(got, np.float64)
+        r64 = np.asarray(ref, np.float64)
+        m64 = float(np.abs(r64).max()) if r64.size else 0.0
+        need = {}
+        if m64 > 0:
+            d64 = np.abs(g64 - r64)
+            for rr in (0.0, 1e-5, 3e-5, 1e-4, 3e-4, 1e-3, 2e-3):
+                need[str(rr)] = float(max((d64 - rr * np.abs(r64)).max(), 0.0)) / m64
+        with open(path, "a") as fh:
+            fh.write(json.dumps({"test": tag, "grad": name, "frac": f, "rel": r, "bar_rel": rel, "bar_frac": frac,
+                                 "need_frac": need, "reduce": os.environ.get("R3DG_BWD_REDUCE", "atomic"),
+                                 "wterms": os.environ.get("R3DG_BWD_WTERMS", "2")}) + "\n")
+    m = float(np.abs(np.asarray(ref)).max()) if np.asarray(ref).size else 0.0
+    assert_close(f"{tag} {name}", got, ref, frac * max(m, 1e-12), rel)
+
+
 import contextlib  # noqa: E402
 
 

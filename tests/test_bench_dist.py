@@ -33,10 +33,14 @@ def test_bench_two_ranks_gloo():
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["unit"] == "Mpix/s"
     assert abs(d["value"] - 2 * 1920 * 1080 / d["ms_per_step"] / 1e3) < 1e-3 * d["value"]
     ex = d["exchange"]
-    assert ex["backend"] == "gloo" and ex["gaussians"] == 20000
-    assert ex["all_reduce_dense22"]["bytes"] == 20000 * 22 * 4 and ex["all_reduce_dense22"]["ms"] > 0
-    assert ex["all_gather_color3"]["bytes_per_rank"] == 20000 * 3 * 4 and ex["all_gather_color3"]["ms"] > 0
+    assert ex["backend"] == "gloo"
+    # the replayed sequence is the step's own: the camera-centre gather + 2 collectives per chunk
+    # (4 chunks: 9), one packed 22-float all-reduce and one 3-float all-gather per Gaussian in total
+    assert d["collectives_per_step"] == ex["collectives_per_step"] == 9
+    assert ex["all_reduce"]["calls"] == 4 and ex["all_gather"]["calls"] == 5
+    assert ex["all_reduce"]["bytes"] == 20000 * 22 * 4 and ex["all_reduce"]["ms"] > 0
+    assert ex["all_gather"]["bytes_per_rank"] == (20000 * 3 + 3) * 4 and ex["all_gather"]["ms"] > 0
     assert ex["compute_only_ms_per_step"] > 0
     assert abs(ex["exposed_exchange_ms_per_step"] - (d["ms_per_step"] - ex["compute_only_ms_per_step"])) < 1e-3
     rf = d["roofline"]
-    assert rf["bound"] == "latency" and rf["extra_bytes"] == 12 * d["config"]["num_rendered"]
+    assert rf["bound"] == "hbm" and rf["binding"] and rf["extra_bytes"] == 12 * d["config"]["num_rendered"]

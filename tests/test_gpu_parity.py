@@ -14,7 +14,8 @@ import pytest
 
 import oracle
 from relightable3dgaussian_amd import synthetic
-from tests._helpers import assert_brdf, assert_close, rows_reduction, hip_backward, hip_forward, tt, upstream_grads
+from tests._helpers import (assert_brdf, assert_close, check_grad, hip_backward, hip_forward, rows_reduction, tt,
+                            upstream_grads)
 
 pytestmark = pytest.mark.gpu
 
@@ -114,45 +115,48 @@ def test_dense_tiles_depth_sort(hip_ext):
     dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=6)
     gh = hip_backward(hip_ext, h, dc, do, dd, df)
     go = oracle.rasterize_backward(o, dc, do, dd, df)
-    for k in ["dL_dmeans2D", "dL_dopacity", "dL_dfeatures", "dL_dmeans3D", "dL_dsh"]:
-        assert_close(k, gh[k], go[k], _grad_tol(go[k]), 2e-3)
+    grad_check("dense_tiles", gh, go, ["dL_dmeans2D", "dL_dopacity", "dL_dfeatures", "dL_dmeans3D", "dL_dsh"])
 
 
-@rows_reduction()
 def test_cull_is_exact(hip_ext):
-    """The per-quadrant footprint skip must not change a single bit (render_fwd.hip)."""
+    """The per-quadrant footprint skip must not change a single bit (render_fwd.hip): forward and
+    rows-reduction backward bitwise, the default atomic backward within assert_hip_runs_agree."""
     scene, cam = synthetic.small_scene(P=5000, S=11, seed=3, width=128, height=96, scale_range=(0.005, 0.3))
-    a = hip_forward(hip_ext, scene, cam, S=11)
-    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11)
-    ga = hip_backward(hip_ext, a, dc, do, dd, df)
+    _cull_on_off(hip_ext, scene, cam)
+
+
+def assert_hip_runs_agree(tag, ga, gb):
+    """Two HIP backward runs on the default atomic flush (order-dependent last bits): within
+    1e-4 |b| + 1e-6 max|b| elementwise (tests/test_gpu_parity.py test_backward_reductions_match_oracle
+    holds the two reductions to the same bar)."""
+    for k in ga:
+        m = max(float(np.abs(gb[k]).max()) if gb[k].size else 0.0, 1e-12)
+        assert_close(f"{tag} {k}", ga[k], gb[k], 1e-6 * m, 1e-4)
+
+
+def _cull_on_off(hip_ext, scene, cam, S=11, seed=1):
+    """Cull on == cull off: forward bitwise; the backward bitwise on the deterministic rows
+    reduction, and on the default atomic flush within assert_hip_runs_agree. Returns the forward,
+    the default (atomic) gradients and the upstream gradients."""
+    a = hip_forward(hip_ext, scene, cam, S=S)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, S, seed=seed)
+    with rows_reduction():  # the two backward runs are compared bit for bit
+        ga = hip_backward(hip_ext, a, dc, do, dd, df)
+    ga_atomic = hip_backward(hip_ext, a, dc, do, dd, df)
     os.environ["R3DG_NO_CULL"] = "1"
     try:
-        b = hip_forward(hip_ext, scene, cam, S=11)
-        gb = hip_backward(hip_ext, b, dc, do, dd, df)
+        b = hip_forward(hip_ext, scene, cam, S=S)
+        with rows_reduction():
+            gb = hip_backward(hip_ext, b, dc, do, dd, df)
+        gb_atomic = hip_backward(hip_ext, b, dc, do, dd, df)
     finally:
         del os.environ["R3DG_NO_CULL"]
     for k in ["color", "opacity", "depth", "feature", "n_contrib", "normal", "surface_xyz"]:
         np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
     for k in ga:
         np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
-
-
-def _cull_on_off(hip_ext, scene, cam, S=11, seed=1):
-    a = hip_forward(hip_ext, scene, cam, S=S)
-    dc, do, dd, df = upstream_grads(cam.height, cam.width, S, seed=seed)
-    with rows_reduction():  # the two backward runs are compared bit for bit
-        ga = hip_backward(hip_ext, a, dc, do, dd, df)
-        os.environ["R3DG_NO_CULL"] = "1"
-        try:
-            b = hip_forward(hip_ext, scene, cam, S=S)
-            gb = hip_backward(hip_ext, b, dc, do, dd, df)
-        finally:
-            del os.environ["R3DG_NO_CULL"]
-    for k in ["color", "opacity", "depth", "feature", "n_contrib", "normal", "surface_xyz"]:
-        np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
-    for k in ga:
-        np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
-    return a, ga, (dc, do, dd, df)
+    assert_hip_runs_agree("cull on/off atomic", ga_atomic, gb_atomic)
+    return a, ga_atomic, (dc, do, dd, df)
 
 
 @pytest.mark.timeout(400)
@@ -171,8 +175,7 @@ def test_cull_exact_needles(hip_ext):
     assert o["num_rendered"] > 1_000_000 and int(o["n_contrib"].max()) > 100
     _check_forward(h, o, 11)
     go = oracle.rasterize_backward(o, dc, do, dd, df)
-    for k in ["dL_dcolors", "dL_dopacity", "dL_dfeatures"]:
-        assert_close(k, gh[k], go[k], _grad_tol(go[k]), 2e-3)
+    grad_check("needles", gh, go, ["dL_dcolors", "dL_dopacity", "dL_dfeatures"])
     # dL/dmean2D = -0.5 W o (a Sdx + b Sdy): for a diagonal needle a ~ -b and Sdx ~ Sdy (pixel
     # offsets of ~1e3 px), so the product cancels by ~1e3 and two fp32 summation orders of the pixel
     # terms (the reference's own atomics included) differ there at ~2e-4 of the largest gradient
@@ -218,9 +221,7 @@ def test_backward_geometry_false(hip_ext):
     df = df * 100.0  # feature grads dominate dL/dalpha, so dropping them is visible
     gh = hip_backward(hip_ext, h, dc, do, dd, df, backward_geometry=False)
     go = oracle.rasterize_backward(o, dc, do, dd, df, backward_geometry=False)
-    for k in ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dfeatures", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
-              "dL_dscales", "dL_drotations"]:
-        assert_close(k, gh[k], go[k], _grad_tol(go[k]), 2e-3)
+    grad_check("bwd_geometry_false", gh, go)
     gt = hip_backward(hip_ext, h, dc, do, dd, df, backward_geometry=True)
     # the feature gradients themselves do not depend on the flag; the geometry gradients do
     np.testing.assert_array_equal(gt["dL_dfeatures"], gh["dL_dfeatures"])
@@ -246,8 +247,25 @@ def test_prefiltered(hip_ext):
     np.testing.assert_array_equal(again["color"].cpu().numpy(), base["color"].cpu().numpy())
 
 
-def _grad_tol(ref):
-    return 2e-5 * max(float(np.abs(ref).max()) if ref.size else 0.0, 1e-12)
+# Raster-gradient bars against the oracle: |HIP - oracle| <= rel |ref| + frac max|ref| per element
+# (tests/_helpers.py check_grad prints the measured max|d|/max|ref| and relative error; DESIGN.md §5
+# records them).
+# Set at <= ~4x the largest error measured on the default build over M1, C2, C3, C4, the C5 view and
+# the small-scene tests (profiles/r05/grad_report.jsonl), with rel = 1e-4 for all. The
+# colour / feature / SH gradients carry the two-term bf16 split of w = alpha T (|w - h - m| <=
+# 2^-16 |w|): ~7.6e-6 of max|ref| measured (the exact three-term split: ~2e-6, the one-term
+# reduction: 3.7e-3 -- test_one_term_reduction_fails_bar); mean2D / opacity / means3D come from the
+# exact moment products (<= 2.5e-7 / 6.3e-7 / 4.3e-7 measured). Round 4's bar was 2e-3 |ref| +
+# 2e-5 max|ref| for all.
+GRAD_BARS = {"dL_dmeans2D": (1e-4, 1e-6), "dL_dopacity": (1e-4, 2.5e-6), "dL_dmeans3D": (1e-4, 1.5e-6),
+             "dL_dcolors": (1e-4, 2e-5), "dL_dfeatures": (1e-4, 2e-5), "dL_dsh": (1e-4, 2e-5),
+             "dL_dcov3D": (1e-4, 2e-5), "dL_dscales": (1e-4, 2e-5), "dL_drotations": (1e-4, 2e-5)}
+
+
+def grad_check(tag, gh, go, keys=None):
+    for k in keys or GRAD_BARS:
+        if k in go and k in gh:
+            check_grad(tag, k, gh[k], go[k], *GRAD_BARS[k])
 
 
 @pytest.mark.parametrize("S", [0, 11, 21, 24, 32])
@@ -258,9 +276,7 @@ def test_backward_matches_oracle(hip_ext, S):
     dc, do, dd, df = upstream_grads(cam.height, cam.width, S)
     gh = hip_backward(hip_ext, h, dc, do, dd, df)
     go = oracle.rasterize_backward(o, dc, do, dd, df)
-    for k in ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dfeatures", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
-              "dL_dscales", "dL_drotations"]:
-        assert_close(k, gh[k], go[k], _grad_tol(go[k]), 2e-3)
+    grad_check(f"bwd S={S}", gh, go)
 
 
 def test_backward_precomputed_colors_and_cov(hip_ext):
@@ -272,8 +288,7 @@ def test_backward_precomputed_colors_and_cov(hip_ext):
     dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=4)
     gh = hip_backward(hip_ext, h, dc, do, dd, df)
     go = oracle.rasterize_backward(o, dc, do, dd, df)
-    for k in ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dfeatures", "dL_dmeans3D", "dL_dcov3D"]:
-        assert_close(k, gh[k], go[k], _grad_tol(go[k]), 2e-3)
+    grad_check("precomputed", gh, go, ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dfeatures", "dL_dmeans3D", "dL_dcov3D"])
     assert np.all(gh["dL_dscales"] == 0) and np.all(gh["dL_drotations"] == 0)
 
 
@@ -290,9 +305,18 @@ def test_backward_deterministic(hip_ext):
         np.testing.assert_array_equal(g1[k], g2[k], err_msg=k)
 
 
-@rows_reduction()
-def test_backward_ex_layouts(hip_ext):
-    """HWC colour / native feature grads (the wrapper's entry) == CHW / planar (reference contract)."""
+@pytest.mark.parametrize("reduce", ["rows", "atomic"])
+def test_backward_ex_layouts(hip_ext, reduce):
+    """HWC colour / native feature grads (the wrapper's entry) == CHW / planar (reference contract):
+    bitwise on the rows reduction, within assert_hip_runs_agree on the default atomic flush."""
+    if reduce == "rows":
+        with rows_reduction():
+            _ex_layouts(hip_ext, exact=True)
+    else:
+        _ex_layouts(hip_ext, exact=False)
+
+
+def _ex_layouts(hip_ext, exact):
     import torch
 
     import relightable3dgaussian_amd as r
@@ -318,8 +342,12 @@ def test_backward_ex_layouts(hip_ext):
     torch.cuda.synchronize()
     names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dfeatures", "dL_dcov3D", "dL_dsh",
              "dL_dscales", "dL_drotations"]
-    for k, v in zip(names, out):
-        np.testing.assert_array_equal(v.cpu().numpy(), g_ref[k], err_msg=k)
+    got = {k: v.cpu().numpy().reshape(g_ref[k].shape) for k, v in zip(names, out)}
+    if exact:
+        for k in names:
+            np.testing.assert_array_equal(got[k], g_ref[k], err_msg=k)
+    else:
+        assert_hip_runs_agree("ex layouts atomic", got, g_ref)
 
 
 def test_empty_and_culled(hip_ext):
@@ -353,7 +381,7 @@ def test_sh_degrees(hip_ext):
         dc, do, dd, df = upstream_grads(cam.height, cam.width, 3, seed=deg)
         gh = hip_backward(hip_ext, h, dc, do, dd, df)
         go = oracle.rasterize_backward(o, dc, do, dd, df)
-        assert_close(f"dL_dsh deg{deg}", gh["dL_dsh"], go["dL_dsh"], _grad_tol(go["dL_dsh"]), 2e-3)
+        grad_check(f"sh deg{deg}", gh, go, ["dL_dsh"])
 
 
 def _keys_vs_oracle(hip_ext, scene, cam, h):
@@ -603,14 +631,9 @@ def test_autograd_wrapper(hip_ext):
     o = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features, sh=scene.sh,
                                  scales=scene.scales, rotations=scene.rotations)
     go = oracle.rasterize_backward(o, dc, do, dd, df)
-    assert_close("means3D.grad", means3D.grad.cpu().numpy(), go["dL_dmeans3D"], _grad_tol(go["dL_dmeans3D"]), 2e-3)
-    assert_close("means2D.grad", means2D.grad.cpu().numpy(), go["dL_dmeans2D"], _grad_tol(go["dL_dmeans2D"]), 2e-3)
-    assert_close("features.grad", feats.grad.cpu().numpy(), go["dL_dfeatures"], _grad_tol(go["dL_dfeatures"]), 2e-3)
-    assert_close("sh.grad", shs.grad.cpu().numpy(), go["dL_dsh"], _grad_tol(go["dL_dsh"]), 2e-3)
-    assert_close("opacity.grad", opac.grad.cpu().numpy(), go["dL_dopacity"], _grad_tol(go["dL_dopacity"]), 2e-3)
-    assert_close("scales.grad", scales.grad.cpu().numpy(), go["dL_dscales"], _grad_tol(go["dL_dscales"]), 2e-3)
-    assert_close("rotations.grad", rots.grad.cpu().numpy(), go["dL_drotations"], _grad_tol(go["dL_drotations"]),
-                 2e-3)
+    got = {"dL_dmeans3D": means3D.grad, "dL_dmeans2D": means2D.grad, "dL_dfeatures": feats.grad, "dL_dsh": shs.grad,
+           "dL_dopacity": opac.grad, "dL_dscales": scales.grad, "dL_drotations": rots.grad}
+    grad_check("autograd", {k: v.cpu().numpy() for k, v in got.items()}, go, list(got))
 
 
 @pytest.mark.parametrize("reduce", ["atomic", "rows"])
@@ -634,9 +657,9 @@ def test_backward_reductions_match_oracle(hip_ext, S, reduce):
             del os.environ["R3DG_BWD_REDUCE"]
         else:
             os.environ["R3DG_BWD_REDUCE"] = prev
+    grad_check(f"reductions {reduce} S={S}", gh, go)
     for k in go:
         if k in gh:
-            assert_close(f"{reduce} {k}", gh[k], go[k], _grad_tol(go[k]), 2e-3)
             assert_close(f"{reduce} vs other {k}", gh[k], gx[k], 1e-6 * max(float(np.abs(gx[k]).max()) if gx[k].size
                                                                            else 0.0, 1e-12), 1e-4)
 
@@ -659,11 +682,20 @@ def test_backward_mfma_matches_dpp_variant(hip_ext, S):
                      1e-3)
 
 
-@rows_reduction()
-def test_backward_chunked_delivery(hip_ext):
-    """Chunked per-Gaussian phase (r3dg_backward_outputs.n_chunks / chunk_done): bitwise the same
-    gradients as one chunk; the callback sees 256-aligned ranges covering every Gaussian in order,
-    with the output tensors (view_parallel.backward_all_reduce overlaps the exchange with it)."""
+@pytest.mark.parametrize("reduce", ["rows", "atomic"])
+def test_backward_chunked_delivery(hip_ext, reduce):
+    """Chunked per-Gaussian phase (r3dg_backward_outputs.n_chunks / chunk_done): the same gradients
+    as one chunk (bitwise on the rows reduction, within assert_hip_runs_agree on the default atomic
+    flush); the callback sees 256-aligned ranges covering every Gaussian in order, with the output
+    tensors (view_parallel.backward_all_reduce overlaps the exchange with it)."""
+    if reduce == "rows":
+        with rows_reduction():
+            _chunked_delivery(hip_ext, exact=True)
+    else:
+        _chunked_delivery(hip_ext, exact=False)
+
+
+def _chunked_delivery(hip_ext, exact):
     scene, cam = synthetic.small_scene(P=3000, S=11, seed=77, width=96, height=80)
     h = hip_forward(hip_ext, scene, cam, S=11)
     dc, do, dd, df = upstream_grads(cam.height, cam.width, 11)
@@ -685,8 +717,12 @@ def test_backward_chunked_delivery(hip_ext):
     assert all(a[2] == b[1] for a, b in zip(seen, seen[1:])) and all(s[1] % 256 == 0 for s in seen)
     names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dfeatures", "dL_dcov3D", "dL_dsh",
              "dL_dscales", "dL_drotations"]
-    for i, k in enumerate(names):
-        np.testing.assert_array_equal(out[i].cpu().numpy().reshape(ref[k].shape), ref[k], err_msg=k)
+    got = {k: out[i].cpu().numpy().reshape(ref[k].shape) for i, k in enumerate(names)}
+    if exact:
+        for k in names:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    else:
+        assert_hip_runs_agree("chunked atomic", got, ref)
 
 
 def _chunked_exchange_worker(rank, world, port, q, mode="views"):
@@ -711,6 +747,10 @@ def _chunked_exchange_worker(rank, world, port, q, mode="views"):
             cam.width, False, False)
     out = view_parallel.backward_all_reduce(r3._C, args, n_chunks=4, sh_exchange=mode)
     torch.cuda.synchronize()
+    # one collective per chunk for the packed dense rows (+ one for the SH part), + the camera gather
+    seq = view_parallel.LAST_COLLECTIVES["sequence"]
+    assert len(seq) == (9 if mode == "views" else 8), seq
+    assert sum(n for k, n in seq if k == "all_reduce") == 2500 * ((11 + 11) if mode == "views" else (22 + 48))
     res = {name: out[i].cpu().numpy() for name, i in view_parallel.GRAD_FIELDS}
     q.put((rank, res, {"means3D": local["dL_dmeans3D"], "sh": local["dL_dsh"], "opacity": local["dL_dopacity"],
                        "scales": local["dL_dscales"], "rotations": local["dL_drotations"],
@@ -777,3 +817,35 @@ def test_sh_rebuild_kernels_match_oracle(hip_ext):
     scale = float(np.abs(ref).max())
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6 * scale)
     np.testing.assert_allclose(got, sum(per_view_sh), rtol=1e-5, atol=1e-6 * scale)
+
+
+def test_one_term_reduction_fails_bar(hip_ext):
+    """The gradient bar can fail: at an M1 crop (480x272 of the M1 camera, the M1 density: 63k
+    Gaussians) the default backward (atomic flush, w split into two bf16 terms) meets GRAD_BARS,
+    while the one-term reduction (R3DG_BWD_WTERMS=1: w truncated to one bf16 term, ~2^-8 relative
+    per product) must violate them on the colour / feature gradients."""
+    cam = synthetic.m1_camera(480, 272)
+    scene = synthetic.m1_scene(P=63_000, S=11, seed=4, cam=cam)
+    o = _oracle_fwd(scene, cam, 11)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=8)
+    go = oracle.rasterize_backward(o, dc, do, dd, df)
+    h = hip_forward(hip_ext, scene, cam, S=11)
+    _check_forward(h, o, 11)
+    grad_check("m1crop", hip_backward(hip_ext, h, dc, do, dd, df), go)
+    os.environ["R3DG_BWD_WTERMS"] = "1"
+    try:
+        g1 = hip_backward(hip_ext, h, dc, do, dd, df)
+    finally:
+        del os.environ["R3DG_BWD_WTERMS"]
+    os.environ["R3DG_BWD_WTERMS"] = "3"
+    try:  # the exact split, for the record (DESIGN.md §5): the default's error above this one is the split's
+        grad_check("m1crop exact-split", hip_backward(hip_ext, h, dc, do, dd, df), go)
+    finally:
+        del os.environ["R3DG_BWD_WTERMS"]
+    failed = []
+    for k in ["dL_dcolors", "dL_dfeatures"]:
+        try:
+            grad_check("m1crop one-term", g1, go, [k])
+        except AssertionError:
+            failed.append(k)
+    assert failed == ["dL_dcolors", "dL_dfeatures"], failed
