@@ -114,11 +114,14 @@ int r3dg_rasterize_gaussians(const r3dg_raster_settings* settings, const r3dg_ga
                              r3dg_alloc_fn binning_alloc, void* binning_ctx, r3dg_alloc_fn image_alloc,
                              void* image_ctx, int* num_rendered, r3dg_stream_t stream);
 
-/* r3dg_rasterize_gaussians with a scratch allocator: the binning's per-workgroup tile counts
- * (up to 8 MiB, [workgroups, tiles] u32, used only until the instances are scattered) come from
- * scratch_alloc, which may hand out stream-ordered memory the caller frees as soon as the call
- * returns (the torch binding passes the caching allocator), instead of the tail of the image
- * state, which lives as long as the autograd context. scratch_alloc NULL = r3dg_rasterize_gaussians. */
+/* r3dg_rasterize_gaussians with a scratch allocator, called once per call: the forward-only
+ * transients -- the binning's per-workgroup tile counts (up to 8 MiB, [workgroups, tiles] u32, used
+ * only until the instances are scattered) and, with non-default splat shaders or post passes, the
+ * shader colour / intermediate-pass records (16 B * P * (record float4s - 2) + 16 B * P) -- come
+ * from scratch_alloc, which may hand out stream-ordered memory the caller frees as soon as the call
+ * returns (the torch binding passes the caching allocator), instead of the tails of the image and
+ * geometry states, which live as long as the autograd context. scratch_alloc NULL =
+ * r3dg_rasterize_gaussians. */
 int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* settings, const r3dg_gaussians* g,
                                 const r3dg_forward_outputs* out, r3dg_alloc_fn geom_alloc, void* geom_ctx,
                                 r3dg_alloc_fn binning_alloc, void* binning_ctx, r3dg_alloc_fn image_alloc,

@@ -422,7 +422,24 @@ def cov3d(scales, rotations, scale_modifier=1.0):
 def _brdf_args(inp):
     b = {k: _f(v) for k, v in inp.items()}
     P = b["base"].shape[0]
-    return b, P, b["incidents"].shape[1], b["env"].shape[1], b["visibility"].shape[1]
+    Si, Sd, Sv = b["incidents"].shape[1], b["env"].shape[1], b["visibility"].shape[1]
+    if max(Si, Sd, Sv) > 16:  # computeSHcoef (render_equation.cu:17-50) yields 16 coefficients
+        raise ValueError(f"render equation: SH coefficient counts must be <= 16 (got {Si}, {Sd}, {Sv})")
+    return b, P, Si, Sd, Sv
+
+
+class brdf_reference_ops:
+    """Context manager: the oracle's render equation evaluates the reference's own operation
+    sequence (render_equation.cu: libm sinf / cosf / expf / powf, every division as written) instead
+    of the shared statements brdf.hip restates bit for bit (oracle/r3dg_oracle.c g_brdf_ref_ops)."""
+
+    def __enter__(self):
+        lib().oracle_set_brdf_ref_ops(ctypes.c_int(1))
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_brdf_ref_ops(ctypes.c_int(0))
+        return False
 
 
 def brdf_forward(inp, sample_num=24, is_training=False, rand=None):

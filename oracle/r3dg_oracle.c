@@ -938,20 +938,43 @@ static void sh_coef3(const float* d, float* coef)
     coef[15] = SH_C3[6] * x * (xx - 3.0f * yy);
 }
 
+/* Two statements of the render equation's arithmetic. Default (0): the operation sequence brdf.hip
+ * evaluates (shared r3dg_sincosf / r3dg_expf_wide, powers as products, one division per shared
+ * denominator) -- the GPU matches it bit for bit. 1: the reference's own sequence as its CUDA source
+ * writes it (render_equation.cu:89-161 / 351-403: libm sinf / cosf / expf / powf, every division
+ * written out, `2 * ray / (2 Ns - 1)` and `2 pi n_d_i / Ns` as written) -- the check of how far
+ * brdf.hip's shared statements sit from the reference's (tests/test_gpu_fullsize.py). */
+static int g_brdf_ref_ops = 0;
+void oracle_set_brdf_ref_ops(int on) { g_brdf_ref_ops = on; }
+
 /* render_equation.cu:89-113 / 581-606: Fibonacci direction rotated to the normal */
 static void fib_dir(const float* n, int ray, int Ns, float rand01, int use_rand, float* dir)
 {
     const float delta = PI_F * (3.0f - sqrtf(5.0f));
-    const float z = 1 - (float)ray * (2.0f / (2 * (float)Ns - 1));
+    const float z = g_brdf_ref_ops ? 1 - 2 * (float)ray / (2 * (float)Ns - 1) : 1 - (float)ray * (2.0f / (2 * (float)Ns - 1));
     const float rad = sqrtf(1 - z * z);
     float theta = delta * ray;
     if (use_rand) theta = rand01 * 2 * PI_F + theta;
     float sn, cs;
-    r3dg_sincosf(theta, &sn, &cs);
+    if (g_brdf_ref_ops) {
+        sn = sinf(theta);
+        cs = cosf(theta);
+    } else {
+        r3dg_sincosf(theta, &sn, &cs);
+    }
     const float y = cs * rad, x = sn * rad;
     float zs[3] = {x, y, z};
     const float v1 = -n[1], v2 = n[0], v3 = 0.f;
     const float v11 = v1 * v1, v22 = v2 * v2, v33 = v3 * v3, v12 = v1 * v2, v13 = v1 * v3, v23 = v2 * v3;
+    if (g_brdf_ref_ops) { /* render_equation.cu:106-112, each term divided */
+        const float c = fmaxf(n[2] + 1, 0.0000001f);
+        float o[3] = {(1 + (-v33 - v22) / c) * zs[0] + (-v3 + v12 / c) * zs[1] + (v2 + v13 / c) * zs[2],
+                      (v3 + v12 / c) * zs[0] + (1 + (-v33 - v11) / c) * zs[1] + (-v1 + v23 / c) * zs[2],
+                      (-v2 + v13 / c) * zs[0] + (v1 + v23 / c) * zs[1] + (1 + (-v22 - v11) / c) * zs[2]};
+        const float norm = sqrtf(fmaxf(0.0000001f, o[0] * o[0] + o[1] * o[1] + o[2] * o[2]));
+        dir[0] = o[0] / norm; dir[1] = o[1] / norm; dir[2] = o[2] / norm;
+        return;
+    }
     /* one division by cp1 and one by norm, then products with the reciprocals (brdf.hip fib_dir; the
      * reference divides each term, render_equation.cu:104-112: within an ulp) */
     const float cp1 = fmaxf(n[2] + 1, 0.0000001f), rc = 1.0f / cp1;
@@ -990,7 +1013,7 @@ static void brdf_eval(int idx, int S_inc, int S_dir, int S_vis, const float* bas
     float h[3] = {d[0] + v[0], d[1] + v[1], d[2] + v[2]};
     s->half_norm = fmaxf(sqrtf(dot3(h, h)), 0.0000001f);
     const float rh = 1.0f / s->half_norm;
-    for (int c = 0; c < 3; ++c) s->half[c] = h[c] * rh;
+    for (int c = 0; c < 3; ++c) s->half[c] = g_brdf_ref_ops ? h[c] / s->half_norm : h[c] * rh;
     s->hdn = fmaxf(dot3(s->half, n), 0.0f);
     s->hdo = fmaxf(dot3(s->half, v), 0.0f);
     s->ndi = fmaxf(dot3(n, d), 0.0f);
@@ -998,16 +1021,17 @@ static void brdf_eval(int idx, int S_inc, int S_dir, int S_vis, const float* bas
     for (int c = 0; c < 3; ++c) s->fd[c] = (1 - metal) * base[c] / PI_F;
     float r2 = fmaxf(rough * rough, 0.0000001f);
     float amp = 1.0f / (r2 * PI_F), sharp = 2.0f / r2;
-    s->D = amp * r3dg_expf_wide(sharp * (s->hdn - 1.0f));
+    s->D = amp * (g_brdf_ref_ops ? expf(sharp * (s->hdn - 1.0f)) : r3dg_expf_wide(sharp * (s->hdn - 1.0f)));
     /* powf(1 - h_d_o, 5) (render_equation.cu:155): CUDA powf's bits are implementation-defined;
      * stated as products (t^2)^2 t, as brdf.hip */
     const float t1 = 1.0f - s->hdo, t2 = t1 * t1;
-    float p5 = t2 * t2 * t1;
+    float p5 = g_brdf_ref_ops ? powf(t1, 5.0f) : t2 * t2 * t1;
     for (int c = 0; c < 3; ++c) {
         float F0 = 0.04f * (1.0f - metal) + base[c] * metal;
         s->F[c] = F0 + (1.0f - F0) * p5;
     }
-    float r2v = (1.0f + rough) * (1.0f + rough) / 8.0f; /* __powf(1 + rough, 2) / 8 (:158) */
+    float r2v = g_brdf_ref_ops ? powf(1.0f + rough, 2.0f) / 8.0f
+                               : (1.0f + rough) * (1.0f + rough) / 8.0f; /* __powf(1 + rough, 2) / 8 (:158) */
     s->V = (0.5f / fmaxf(s->ndi * (1 - r2v) + r2v, 0.0000001f)) * (0.5f / fmaxf(s->ndo * (1 - r2v) + r2v, 0.0000001f));
     for (int c = 0; c < 3; ++c) s->fs[c] = s->D * s->F[c] * s->V;
 }
@@ -1028,7 +1052,7 @@ void oracle_render_equation_forward(int P, int S_inc, int S_dir, int S_vis, cons
             brdf_sample s;
             brdf_eval(idx, S_inc, S_dir, S_vis, base + 3 * idx, rough[idx], metal[idx], normals + 3 * idx,
                       viewdirs + 3 * idx, inc, dir_shs, vis_shs, d, coef, &s);
-            float tmp = s.ndi * (2.0f * PI_F / (float)Ns);
+            float tmp = g_brdf_ref_ops ? 2.0f * PI_F * s.ndi / (float)Ns : s.ndi * (2.0f * PI_F / (float)Ns);
             for (int c = 0; c < 3; ++c) {
                 float tr = s.light[c] * tmp;
                 acc_p[c] += (s.fd[c] + s.fs[c]) * tr;
@@ -1058,7 +1082,7 @@ void oracle_render_equation_forward_complex(int P, int S_inc, int S_dir, int S_v
             brdf_sample s;
             brdf_eval(idx, S_inc, S_dir, S_vis, base + 3 * idx, rough[idx], metal[idx], normals + 3 * idx,
                       viewdirs + 3 * idx, inc, dir_shs, vis_shs, d, coef, &s);
-            float tmp = s.ndi * (2.0f * PI_F / (float)Ns);
+            float tmp = g_brdf_ref_ops ? 2.0f * PI_F * s.ndi / (float)Ns : s.ndi * (2.0f * PI_F / (float)Ns);
             size_t w = (size_t)idx * Ns + r;
             for (int c = 0; c < 3; ++c) {
                 float g = s.vis * s.global[c];
@@ -1095,6 +1119,10 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
                                      float* d_base, float* d_rough, float* d_metal, float* d_normal, float* d_view,
                                      float* d_inc, float* d_dir, float* d_vis)
 {
+    if (S_dir > 16 || S_inc > 16 || S_vis > 16) { /* computeSHcoef gives 16 coefficients (degree 3) */
+        fprintf(stderr, "oracle_render_equation_backward: S_dir / S_inc / S_vis must be <= 16\n");
+        abort();
+    }
     const float K = 2.0f * PI_F / (float)Ns;
     /* dL_ddirect_shs: the reference's racy float += over every (Gaussian, sample) (:443-445) has
      * no defined value; here it is the exact sum (double accumulation, rounded once), which any
@@ -1115,8 +1143,9 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             brdf_eval(idx, S_inc, S_dir, S_vis, b, rough_i, metal_i, n, v, inc, dir_shs, vis_shs, d, coef, &s);
             float r2 = fmaxf(rough_i * rough_i, 0.0000001f);
             float amp = 1.0f / (r2 * PI_F), sharp = 2.0f / r2;
-            float e_amp = r3dg_expf_wide(sharp * (s.hdn - 1.0f));
-            float r2v = (1.0f + rough_i) * (1.0f + rough_i) / 8.0f; /* powf(1 + rough, 2) / 8 (:359) */
+            float e_amp = g_brdf_ref_ops ? expf(sharp * (s.hdn - 1.0f)) : r3dg_expf_wide(sharp * (s.hdn - 1.0f));
+            float r2v = g_brdf_ref_ops ? powf(1.0f + rough_i, 2.0f) / 8.0f
+                                       : (1.0f + rough_i) * (1.0f + rough_i) / 8.0f; /* powf(1 + rough, 2) / 8 (:359) */
             float den1 = fmaxf(s.ndi * (1 - r2v) + r2v, 0.0000001f);
             float den2 = fmaxf(s.ndo * (1 - r2v) + r2v, 0.0000001f);
             float g1 = 0.5f / den1, g2 = 0.5f / den2;
@@ -1145,7 +1174,7 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             float drough = dr2 * 2.0f * rough_i;
             /* powf(1 - h_d_o, 5 / 4) (:394-395) as products, as brdf_eval */
             const float t1 = 1.0f - s.hdo, t2 = t1 * t1;
-            float p4 = t2 * t2, p5 = p4 * t1;
+            float p4 = g_brdf_ref_ops ? powf(t1, 4.0f) : t2 * t2, p5 = g_brdf_ref_ops ? powf(t1, 5.0f) : p4 * t1;
             float dF0[3], dhdo = 0;
             for (int c = 0; c < 3; ++c) {
                 float F0 = 0.04f * (1.0f - metal_i) + b[c] * metal_i;
@@ -1156,7 +1185,8 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             for (int c = 0; c < 3; ++c) dbase[c] += metal_i * dF0[c];
             dmetal += (b[0] - 0.04f) * dF0[0] + (b[1] - 0.04f) * dF0[1] + (b[2] - 0.04f) * dF0[2];
             float dg1 = dV * g2, dg2 = dV * g1;
-            float dden1 = -2.0f * (g1 * g1) * dg1, dden2 = -0.5f / (den2 * den2) * dg2; /* -0.5/den1^2 = -2 g1^2 */
+            float dden1 = g_brdf_ref_ops ? -0.5f / (den1 * den1) * dg1 : -2.0f * (g1 * g1) * dg1; /* -0.5/den1^2 = -2 g1^2 */
+            float dden2 = -0.5f / (den2 * den2) * dg2;
             dndi = dden1 * (1 - r2v); /* overwrite: render_equation.cu:403 (bug-compatible) */
             float dndo = dden2 * (1 - r2v);
             float dr2v = (1.0f - s.ndi) * dden1 + (1.0f - s.ndo) * dden2;
@@ -1167,13 +1197,13 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             if (s.ndi > 0.0f) for (int c = 0; c < 3; ++c) dn[c] += d[c] * dndi;
             if (s.ndo > 0.0f) for (int c = 0; c < 3; ++c) { dn[c] += v[c] * dndo; dv[c] += n[c] * dndo; }
             const float rh = 1.0f / s.half_norm;
-            for (int c = 0; c < 3; ++c) dv[c] += dhalf[c] * rh;
+            for (int c = 0; c < 3; ++c) dv[c] += g_brdf_ref_ops ? dhalf[c] / s.half_norm : dhalf[c] * rh;
             float dglob[3], dvis_s = 0;
             for (int c = 0; c < 3; ++c) dglob[c] = dli[c] * s.vis;
             for (int c = 0; c < 3; ++c) dvis_s += dli[c] * s.global[c];
             for (int i = 0; i < S_vis; ++i) d_vis[(size_t)idx * S_vis + i] = fmaf(dvis_s, coef[i], d_vis[(size_t)idx * S_vis + i]);
             /* clamp checks after fmaxf never fire (render_equation.cu:440-449, bug-compatible) */
-            for (int i = 0; i < S_dir && i < 16; ++i)
+            for (int i = 0; i < S_dir; ++i)
                 for (int c = 0; c < 3; ++c) ddir_acc[i * 3 + c] += (double)dglob[c] * (double)coef[i];
             for (int i = 0; i < S_dir; ++i) /* loop bound S_direct, render_equation.cu:450 */
                 for (int c = 0; c < 3; ++c)
@@ -1187,7 +1217,7 @@ void oracle_render_equation_backward(int P, int S_inc, int S_dir, int S_vis, con
             d_rough[idx] += drough;
         }
     }
-    for (int i = 0; i < S_dir && i < 16; ++i)
+    for (int i = 0; i < S_dir; ++i)
         for (int c = 0; c < 3; ++c) d_dir[i * 3 + c] += (float)ddir_acc[i * 3 + c];
 }
 

@@ -499,30 +499,54 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     // the geometry state proper (the backward never reads them)
     const size_t geom_bytes = geom_state_bytes((size_t)P, S);
     const size_t M3 = (size_t)3 * (g->sh ? s->M : 0);
-    const size_t work_floats = work_copies ? (size_t)P * (3 + 3 + 4 + 1 + M3 + S) : 0;
+    // Only the inputs an active shader writes get a working copy (the others are read in place;
+    // shaders.hip): positions (SH ExpPos / Heartbeat / GaussDissolve), scales (ExpPos / Heartbeat /
+    // CullHalf), opacity (CullHalf / GaussDissolve), the SH block (GaussDissolve: sh0), features
+    // (splat CrackNoRecon / RoughnessOnly / QuantizeLight); rotations never. The reference copies all
+    // six (rasterize_points.cu:117-122): results are the same, the copies were 0.11 ms per frame at
+    // M1 with S = 21.
+    auto sh_on = [&](int id) { return sh_active && id < (int)shm->counts.size() && shm->counts[id] > 0; };
+    auto sp_on = [&](int id) { return splat_active && id < (int)spm->counts.size() && spm->counts[id] > 0; };
+    const bool w_pos = sh_on(kShExpPos) || sh_on(kShHeartbeat) || sh_on(kShGaussDissolve);
+    const bool w_scale = sh_on(kShExpPos) || sh_on(kShHeartbeat) || sh_on(kShCullHalf);
+    const bool w_opac = sh_on(kShCullHalf) || sh_on(kShGaussDissolve);
+    const bool w_sh = sh_on(kShGaussDissolve);
+    const bool w_feat = sp_on(kSpCrackNoRecon) || sp_on(kSpRoughnessOnly) || sp_on(kSpQuantizeLight);
+    const size_t work_floats = work_copies ? (size_t)P * ((w_pos ? 3 : 0) + (w_scale ? 3 : 0) + (w_opac ? 1 : 0) +
+                                                         (w_sh ? M3 : 0) + (w_feat ? S : 0))
+                                           : 0;
+    // the splat shaders that read the intermediate depth image (Crack, CrackNoRecon: the depth at the
+    // mean pixel); without them the pre-shader intermediate pass only yields a stencil of zeros (every
+    // stencil opacity is still InitializeStencil's 0 there, so every stencil alpha is 0) and the
+    // blend overwrites its depth, so it is replaced by a memset
+    const bool inter_pre = sp_on(kSpCrack) || sp_on(kSpCrackNoRecon);
     const size_t post_floats = post_blur ? (size_t)3 * H * W : 0;  // BlurLighting's incident-light snapshot
     // the splat shaders' colour as one float4 per Gaussian (16-B aligned, after the other extras)
     const size_t shrec_off = (work_floats + post_floats + 3) & ~(size_t)3;
     const size_t shrec_floats = splat_active ? 4 * (size_t)P * (record_f4(S) - 2) : 0;
     // the intermediate depth / stencil pass's packed per-Gaussian record (launch_intermediate)
     const size_t inter_floats = (splat_active || !post_ids.empty()) ? 4 * (size_t)P : 0;
-    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * (shrec_off + shrec_floats + inter_floats));
-    // with a scratch allocator the binning's tile counts are transient (needed only until the
-    // scatter), not part of the image state autograd keeps alive until the backward
-    const bool hist_scratch = scratch_alloc != nullptr && P > 0;
-    void* img_base = image_alloc(image_ctx, image_state_bytes(H, W, !hist_scratch));
-    uint32_t* hist_base = hist_scratch ? (uint32_t*)scratch_alloc(scratch_ctx, 4 * bin_hist_count((size_t)T)) : nullptr;
-    if (!geom_base || !img_base || (hist_scratch && !hist_base)) {
+    // With a scratch allocator (one call, stream-ordered memory freed when the call returns) the
+    // forward-only transients live there instead of in the state autograd keeps until the
+    // backward: the binning's per-workgroup tile counts (needed until the scatter) and the splat
+    // shaders' / intermediate pass's per-Gaussian records (112 MB at 1M Gaussians with S = 21).
+    const bool use_scratch = scratch_alloc != nullptr && P > 0;
+    const size_t rec_bytes = sizeof(float) * (shrec_floats + inter_floats);
+    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * shrec_off + (use_scratch ? 0 : rec_bytes));
+    void* img_base = image_alloc(image_ctx, image_state_bytes(H, W, !use_scratch));
+    const size_t hist_bytes = (4 * bin_hist_count((size_t)T) + 255) & ~(size_t)255;
+    char* scratch_base = use_scratch ? (char*)scratch_alloc(scratch_ctx, hist_bytes + rec_bytes) : nullptr;
+    if (!geom_base || !img_base || (use_scratch && !scratch_base)) {
         set_error("rasterize_gaussians: state allocation failed");
         return R3DG_ERR_ALLOC;
     }
+    uint32_t* hist_base = use_scratch ? reinterpret_cast<uint32_t*>(scratch_base) : nullptr;
+    char* rec_base = use_scratch ? scratch_base + hist_bytes
+                                 : static_cast<char*>(geom_base) + geom_bytes + sizeof(float) * shrec_off;
     GeomState geom = geom_state_from(geom_base, (size_t)P, S);
-    float4* shader_rec =
-        splat_active ? reinterpret_cast<float4*>(static_cast<char*>(geom_base) + geom_bytes + sizeof(float) * shrec_off)
-                     : nullptr;
-    float4* inter_rec = inter_floats ? reinterpret_cast<float4*>(static_cast<char*>(geom_base) + geom_bytes +
-                                                                 sizeof(float) * (shrec_off + shrec_floats))
-                                     : nullptr;
+    float4* shader_rec = splat_active ? reinterpret_cast<float4*>(rec_base) : nullptr;
+    float4* inter_rec = inter_floats ? reinterpret_cast<float4*>(rec_base + sizeof(float) * shrec_floats) : nullptr;
+    const bool hist_scratch = use_scratch;
     ImageState img = carve_image((uintptr_t)img_base, H, W, nullptr, !hist_scratch);
     if (hist_scratch) img.bin_hist = hist_base;
     int* radii = out->radii ? out->radii : geom.internal_radii;
@@ -538,18 +562,18 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     if (work_copies) {
         float* w = reinterpret_cast<float*>(static_cast<char*>(geom_base) + geom_bytes);
         hipError_t ce = hipSuccess;
-        auto copy = [&](const float* src, size_t n) -> float* {
+        auto copy = [&](const float* src, size_t n, bool written) -> float* {
+            if (!written) return const_cast<float*>(src);  // read in place: no active shader writes it
             float* d = w;
             w += n;
             if (src && n && ce == hipSuccess) ce = hipMemcpyAsync(d, src, sizeof(float) * n, hipMemcpyDeviceToDevice, st);
             return src ? d : nullptr;
         };
-        means3D = copy(g->means3D, 3 * (size_t)P);
-        scales = copy(g->scales, 3 * (size_t)P);
-        rotations = copy(g->rotations, 4 * (size_t)P);
-        opacity = copy(g->opacity, (size_t)P);
-        shs = copy(g->sh, M3 * P);
-        feats = copy(g->features, (size_t)S * P);
+        means3D = copy(g->means3D, 3 * (size_t)P, w_pos);
+        scales = copy(g->scales, 3 * (size_t)P, w_scale);
+        opacity = copy(g->opacity, (size_t)P, w_opac);
+        shs = copy(g->sh, M3 * P, w_sh);
+        feats = copy(g->features, (size_t)S * P, w_feat);
         R3DG_CHECK_HIP(ce);
     }
     // InitializeStencil (rasterizer_impl.cu:203-209): only the shaders and the intermediate
@@ -686,7 +710,11 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     if (splat_active) {
         // the splat shaders read the intermediate depth / stencil images
         R3DG_REQUIRE(out->depth && out->stencil, "rasterize_gaussians: splat shaders need depth and stencil outputs");
-        R3DG_CHECK_HIP(launch_intermediate(ia, P, radii, st));
+        if (inter_pre) {
+            R3DG_CHECK_HIP(launch_intermediate(ia, P, radii, st));
+        } else {
+            R3DG_CHECK_HIP(hipMemsetAsync(out->stencil, 0, sizeof(float) * (size_t)H * W, st));
+        }
         R3DG_CHECK_LAUNCH(s->debug, st);
         for (int id = 0; id < (int)spm->counts.size(); ++id) {  // RunSplatShaders (forward.cu:907-971)
             if (spm->counts[id] == 0) continue;

@@ -477,8 +477,9 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         float dx0 = go, dx1 = 0.f;
 #pragma unroll
         for (int c2 = 0; c2 < 2 * NA4; ++c2) {
-            dx0 = __builtin_fmaf(v[2 * c2], gp[c2].x, dx0);
-            dx1 = __builtin_fmaf(v[2 * c2 + 1], gp[c2].y, dx1);
+            // (the row's 4 + SMAX real values only: SMAX = 11 skips the pad channel's FMA)
+            if (2 * c2 < 4 + SMAX) dx0 = __builtin_fmaf(v[2 * c2], gp[c2].x, dx0);
+            if (2 * c2 + 1 < 4 + SMAX) dx1 = __builtin_fmaf(v[2 * c2 + 1], gp[c2].y, dx1);
         }
         const float d = dx0 + dx1;
         const float diff = d - u;
@@ -809,7 +810,9 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         const long long tw0 = wall_clock64();
 #endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifndef R3DG_EXP_NOBARRIER  // timing experiment only (results invalid): no cross-wave batch sync
         __syncthreads();
+#endif
 #ifdef R3DG_EXP_COUNT
         t_wait += wall_clock64() - tw0;
 #endif
@@ -833,18 +836,22 @@ static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
     // DMA-staged MFMA kernel. Both write the same partial rows (the forward's contribution set).
     const char* e = getenv("R3DG_BWD");  // read per launch: tests switch it at run time
     const bool dpp = e && e[0] == 'd';
-    // R3DG_BWD_WTERMS=1 / 3 (S in 9..12, atomic sums only; refused otherwise): w in one bf16 term,
+    // R3DG_BWD_WTERMS=1 / 3 (S in 9..11, atomic sums only; refused otherwise): w in one bf16 term,
     // the inexact reduction the gradient parity bar must reject, or in three (exact products), the
     // reference point of the default two-term split's error (tests/test_gpu_parity.py)
     const char* wt = getenv("R3DG_BWD_WTERMS");
     const int wterms = wt && wt[0] ? wt[0] - '0' : 0;
     const int grid = padded_tile_grid(a.num_tiles);
     if (wterms) {
-        if (SMAX != 12 || !a.sums_atomic || dpp || (wterms != 1 && wterms != 3)) return hipErrorInvalidValue;
-        if (wterms == 1)
-            launch_kernel(render_bwd_glds_kernel<SMAX, true, 1>, dim3(grid), dim3(kBlock), stream, a);
-        else
-            launch_kernel(render_bwd_glds_kernel<SMAX, true, 3>, dim3(grid), dim3(kBlock), stream, a);
+        if constexpr (SMAX == 11) {
+            if (!a.sums_atomic || dpp || (wterms != 1 && wterms != 3)) return hipErrorInvalidValue;
+            if (wterms == 1)
+                launch_kernel(render_bwd_glds_kernel<SMAX, true, 1>, dim3(grid), dim3(kBlock), stream, a);
+            else
+                launch_kernel(render_bwd_glds_kernel<SMAX, true, 3>, dim3(grid), dim3(kBlock), stream, a);
+        } else {
+            return hipErrorInvalidValue;
+        }
     } else if (dpp)
         launch_kernel(render_bwd_dpp_kernel<SMAX>, dim3(grid), dim3(kBlock), stream, a);
     else if (a.sums_atomic)
@@ -859,6 +866,7 @@ hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t stream) {
     if (a.S == 0) return launch_bwd_s<0>(a, stream);
     if (a.S <= 4) return launch_bwd_s<4>(a, stream);
     if (a.S <= 8) return launch_bwd_s<8>(a, stream);
+    if (a.S <= 11) return launch_bwd_s<11>(a, stream);  // M1 / C3 (S = 11): no pad-channel FMA
     if (a.S <= 12) return launch_bwd_s<12>(a, stream);
     if (a.S <= 16) return launch_bwd_s<16>(a, stream);
     if (a.S <= 24) return launch_bwd_s<24>(a, stream);

@@ -322,6 +322,7 @@ hipError_t launch_render_forward(const RenderFwdArgs& a, bool shader, hipStream_
     if (a.S == 0) return launch_fwd_s<0>(a, shader, stream);
     if (a.S <= 4) return launch_fwd_s<4>(a, shader, stream);
     if (a.S <= 8) return launch_fwd_s<8>(a, shader, stream);
+    if (a.S <= 11) return launch_fwd_s<11>(a, shader, stream);  // M1 / C3 (S = 11): no pad-channel FMA
     if (a.S <= 12) return launch_fwd_s<12>(a, shader, stream);
     if (a.S <= 16) return launch_fwd_s<16>(a, shader, stream);
     if (a.S <= 24) return launch_fwd_s<24>(a, shader, stream);

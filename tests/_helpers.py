@@ -149,6 +149,37 @@ def check_grad(tag, name, got, ref, rel, frac):
     assert_close(f"{tag} {name}", got, ref, frac * max(m, 1e-12), rel)
 
 
+def assert_brdf_refops(name, got, ref, grad=False, summed=False, sensitivity=None):
+    """The render equation against the oracle run with the REFERENCE's operation sequence
+    (oracle.brdf_reference_ops: libm sinf / cosf / expf / powf, divisions as written) instead of
+    the shared statements brdf.hip restates bit for bit: the distance from this build's arithmetic
+    to the reference's. Round 3's bars (before the shared statements): outputs 2e-4 abs + 1e-3 rel,
+    gradients 2e-5 max|ref| + 1e-3 rel (the summed environment gradient 5e-4 max|ref|).
+    `sensitivity(gaussians) -> {gaussian: spread}`: for the few Gaussians outside the bar, the spread
+    of the reference-ops oracle itself when its sample directions move by one ulp; such an element
+    passes within 4x that spread (ill-conditioned: the sharp lobe at the roughness floor amplifies an
+    ulp ~500x and d_rough cancels large terms). At most 1e-4 of the Gaussians may need it."""
+    got = np.asarray(got)
+    ref = np.asarray(ref)
+    d = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+    m = float(np.abs(ref).max()) if ref.size else 0.0
+    atol = ((5e-4 if summed else 2e-5) * max(m, 1e-9)) if grad else 2e-4
+    bar = atol + 1e-3 * np.abs(ref.astype(np.float64))
+    bad = d > bar
+    print(f"brdf vs reference ops {name}: max abs diff {d.max() if d.size else 0:.3e} (max|ref| {m:.3e}), "
+          f"{int(bad.sum())} outside round 3's bar")
+    if bad.any() and sensitivity is not None and not summed:
+        gs = sorted(set(int(i) for i in np.argwhere(bad)[:, 0]))
+        assert len(gs) <= max(1, int(1e-4 * ref.shape[0])), (name, len(gs))
+        spread = sensitivity(gs)
+        for g in gs:
+            dg = d[g].max()
+            print(f"  {name} Gaussian {g}: diff {dg:.3e}, oracle ulp spread {spread[g]:.3e}")
+            assert dg <= 4.0 * spread[g] + bar[g].max(), (name, g, dg, spread[g])
+        return
+    assert_close(name, got, ref, atol, 1e-3)
+
+
 import contextlib  # noqa: E402
 
 

@@ -16,7 +16,7 @@ import pytest
 
 import oracle
 from relightable3dgaussian_amd import synthetic
-from tests._helpers import assert_brdf, assert_close, hip_backward, hip_forward, tt, upstream_grads
+from tests._helpers import assert_brdf, assert_brdf_refops, hip_backward, hip_forward, tt, upstream_grads
 from tests.test_gpu_parity import _check_forward, _oracle_fwd, grad_check
 
 pytestmark = pytest.mark.gpu
@@ -97,6 +97,33 @@ def test_c3_training_step_full_size(hip_ext):
     ob = oracle.brdf_backward(inp, of["incident_dirs"], gp, gd, 24)
     for k, v in zip(["base", "rough", "metal", "normals", "viewdirs", "incidents", "env", "visibility"], out):
         assert_brdf("d_" + k, v.cpu().numpy(), ob[k], summed=k == "env")
+    # against the reference's own operation sequence (libm sin / cos / exp / pow, divisions as
+    # written), at round 3's bars: the shared statements stay within them at full size
+    with oracle.brdf_reference_ops():
+        rf = oracle.brdf_forward(inp, 24, True, rnd)
+        rb = oracle.brdf_backward(inp, rf["incident_dirs"], gp, gd, 24)
+    for k, v in zip(["pbr", "incident_dirs", "diffuse_light"], (pbr, dirs, dl)):
+        assert_brdf_refops(k, v.cpu().numpy(), rf[k])
+    out = hip_ext.render_equation_backward(*_brdf_tensors(inp), 24, tt(rf["incident_dirs"]), tt(gp), tt(gd), False)
+
+    def spread(gs, key):
+        """The reference-ops oracle's own spread on Gaussians gs when their sample directions move
+        by one ulp (random direction, four draws)."""
+        sub = {k: (v[gs] if v.shape[0] == P else v) for k, v in inp.items()}
+        dirs = rf["incident_dirs"][gs]
+        rng2 = np.random.default_rng(5)
+        with oracle.brdf_reference_ops():
+            base = oracle.brdf_backward(sub, dirs, gp[gs], gd[gs], 24)[key]
+            s = np.zeros(len(gs))
+            for _ in range(4):
+                pert = np.nextafter(dirs, np.where(rng2.random(dirs.shape) < 0.5, -np.inf, np.inf).astype(np.float32))
+                g2 = oracle.brdf_backward(sub, pert.astype(np.float32), gp[gs], gd[gs], 24)[key]
+                s = np.maximum(s, np.abs(g2.astype(np.float64) - base).reshape(len(gs), -1).max(1))
+        return dict(zip(gs, s))
+
+    for k, v in zip(["base", "rough", "metal", "normals", "viewdirs", "incidents", "env", "visibility"], out):
+        assert_brdf_refops("d_" + k, v.cpu().numpy(), rb[k], grad=True, summed=k == "env",
+                           sensitivity=lambda gs, k=k: spread(gs, k))
 
 
 @pytest.mark.timeout(600)
@@ -161,3 +188,7 @@ def test_c2_brdf_complex_full_size(hip_ext):
         # (shared sin / cos / exp, contraction off), so the Gaussians at the 0.05 roughness floor --
         # whose sharp lobe amplified an ulp of direction into 2e-4 in round 3 -- match as well
         assert_brdf(k, h[k], o[k])
+    with oracle.brdf_reference_ops():  # the reference's own operation sequence, round 3's bars
+        r = oracle.brdf_forward_complex(inp, 24)
+    for k in names:
+        assert_brdf_refops(k, h[k], r[k])

@@ -105,6 +105,29 @@ def test_brdf_backward_matches_reference_autograd():
         _close("d_" + k, o[k], ref, 1e-5 * float(np.abs(ref).max()) + 1e-6, 1e-3)
 
 
+def test_brdf_reference_ops_variant_matches_reference():
+    """The oracle's second statement of the render equation -- the reference CUDA's own operation
+    sequence (libm sinf / cosf / expf / powf, divisions as written; oracle.brdf_reference_ops) --
+    is held to the same reference fixtures as the shared statements brdf.hip restates; an SH
+    coefficient count above 16 (computeSHcoef's degree 3) is refused, not truncated."""
+    g = _gold("brdf_pi5.npz")
+    with oracle.brdf_reference_ops():
+        o = oracle.brdf_forward_complex(_brdf_inp(g), int(g["sample_num"]))
+        inp = _brdf_inp(g, "g_")
+        ones = np.ones((inp["base"].shape[0], 3), np.float32)
+        b = oracle.brdf_backward(inp, g["g_incident_dirs"], ones, ones, int(g["sample_num"]))
+    for k in ["pbr", "diffuse_light", "incident_dirs", "incident_lights", "local_incident_lights",
+              "global_incident_lights", "incident_visibility"]:
+        _close(k, o[k], g[k], 2e-5, 1e-4)
+    for k in ["base", "rough", "metal", "incidents", "visibility", "env"]:
+        ref = g["grad_" + k]
+        _close("d_" + k, b[k], ref, 1e-5 * float(np.abs(ref).max()) + 1e-6, 1e-3)
+    big = dict(_brdf_inp(g))
+    big["env"] = np.zeros((1, 25, 3), np.float32)
+    with pytest.raises(ValueError, match="<= 16"):
+        oracle.brdf_forward(big, 24)
+
+
 def test_brdf_python_pi_differs_only_by_constant():
     """The np.pi fixture and the 3.14159f fixture differ by a small amount: documents why the
     pi5 fixture is the one the CUDA-path oracle is held to."""

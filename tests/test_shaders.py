@@ -335,3 +335,24 @@ def test_shader_validation_is_loud(hip_ext):
     ids = np.full(scene.P, oracle.SP_WIREFRAME)
     with pytest.raises(RuntimeError, match="21"):            # addresses features 6..8 with S = 11
         hip_forward(hip_ext, scene, cam, S=11, splat_manager=_manager(hip_ext, 1, ids))
+
+
+@pytest.mark.gpu
+def test_partial_shader_sets_match_oracle(hip_ext):
+    """Only the inputs an active shader writes get working copies, and the pre-shader intermediate
+    pass runs only when a depth-reading splat shader (Crack, CrackNoRecon) is active
+    (rasterizer.hip): with SH CullHalf + default and splat Wireframe / QuantizeLight + default, every
+    output still matches the oracle (which copies everything and always runs the pass)."""
+    scene, cam = shader_scene(P=4000, seed=15)
+    tex = golden_textures()
+    rng = np.random.default_rng(3)
+    sh_ids = rng.choice([oracle.SH_NAMES.index("CullHalf"), oracle.SH_NAMES.index("ShDefault")], scene.P)
+    sp_ids = rng.choice([oracle.SP_WIREFRAME, oracle.SP_QUANTIZELIGHT, oracle.SP_DEFAULT], scene.P)
+    texm = _gpu_textures(hip_ext, tex)
+    h = hip_forward(hip_ext, scene, cam, time=700.0, texture_manager=texm, sh_manager=_manager(hip_ext, 0, sh_ids),
+                    splat_manager=_manager(hip_ext, 1, sp_ids))
+    T = {k: oracle.Texture(v, mode=4) for k, v in tex.items()}
+    o = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features, sh=scene.sh, scales=scene.scales,
+                                 rotations=scene.rotations, sh_shaders=sh_ids, splat_shaders=sp_ids, textures=T,
+                                 error_texture=T["Error"], time=700.0)
+    _check(h, o)

@@ -338,3 +338,53 @@ def test_gpu_step_absent_matches_oracle(gold, hip_ext):
     for k in range(3):
         for n in want[k]:
             _close(got[k][n].reshape(st.P, -1), want[k][n].reshape(st.P, -1), f"step {k} {n}")
+
+
+def test_absent_group_matches_torch_adam_cpu(gold):
+    """the `absent` semantics against torch.optim.Adam itself (single-tensor, CPU), not a
+    hand-written Adam: two steps, every group with a gradient in the first, "normal" with
+    grad=None in the second. param, exp_avg, exp_avg_sq and state['step'] per group must equal the
+    trainer's (CPU Adam of oracle/train_oracle.py, per-group step counts): step counts exactly,
+    values to a few ulp (torch fuses its multiply-adds), and the absent group's param / exp_avg /
+    exp_avg_sq untouched by the step it skipped, bit for bit in both."""
+    import torch
+
+    from relightable3dgaussian_amd import trainer
+
+    tens = _tensors(gold)
+    st = trainer.GaussianTrainState.from_tensors(tens)
+    st.training_setup(_opt_args(), spatial_lr_scale=2.5)
+    names = [n for n, _ in st.groups]
+    params = {n: torch.nn.Parameter(st.view(n).clone()) for n in names}
+    opt = torch.optim.Adam([{"params": [params[n]], "lr": lr, "name": n} for n, lr in zip(names, st.lrs)],
+                           lr=0.0, eps=1e-15, foreach=False)
+    rng = np.random.default_rng(11)
+    kept = {}
+    for k in range(2):
+        if k == 1:
+            kept = {"p": st.view("normal").clone(), "m": st._view(st.exp_avg, "normal").clone(),
+                    "v": st._view(st.exp_avg_sq, "normal").clone(), "tp": params["normal"].detach().clone(),
+                    "tm": opt.state[params["normal"]]["exp_avg"].clone()}
+        for n in names:
+            g = torch.from_numpy(rng.normal(size=tuple(params[n].shape)).astype(np.float32) * 1e-2)
+            if k == 1 and n == "normal":
+                params[n].grad = None
+                continue
+            params[n].grad = g.clone()
+            st.grad_view(n).copy_(g)
+        opt.step()
+        st.step(adam_fn=_cpu_adam_groups, absent=("normal",) if k == 1 else ())
+    for i, n in enumerate(names):
+        s = opt.state[params[n]]
+        # torch's CPU lerp / addcdiv fuse their multiply-adds (one rounding fewer than the oracle's
+        # statements): values agree to a few ulp; the step counts exactly
+        np.testing.assert_allclose(st.view(n).numpy(), params[n].detach().numpy(), rtol=1e-6, atol=1e-9, err_msg=n)
+        for mine, ref in ((st._view(st.exp_avg, n), s["exp_avg"]), (st._view(st.exp_avg_sq, n), s["exp_avg_sq"])):
+            np.testing.assert_allclose(mine.numpy(), ref.numpy(), rtol=1e-6, atol=1e-6 * float(ref.abs().max()),
+                                       err_msg=n)
+        assert st.group_steps[i] == int(s["step"]), n
+    assert st.group_steps[names.index("normal")] == 1 and st.group_steps[names.index("xyz")] == 2
+    assert torch.equal(st.view("normal"), kept["p"]) and torch.equal(st._view(st.exp_avg, "normal"), kept["m"])
+    assert torch.equal(st._view(st.exp_avg_sq, "normal"), kept["v"])
+    assert torch.equal(params["normal"].detach(), kept["tp"])
+    assert torch.equal(opt.state[params["normal"]]["exp_avg"], kept["tm"])
