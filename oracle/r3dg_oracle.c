@@ -71,11 +71,13 @@ static void get_rect(float px, float py, int max_radius, int gx, int gy, int* rm
 }
 
 /* forward.cu:468 / backward.cu:526: -0.5f * (a dx^2 + c dy^2) - b dx dy as one fixed FMA pattern
- * (the HIP kernels' gauss_power, r3dg_common.h). */
+ * (the HIP kernels' gauss_power, r3dg_common.h): with the staged conic (A, B, C) = (-a/2, -b, -c/2)
+ * (exact scalings, preprocess_kernel's render records), dx (A dx + B dy) + C dy^2. */
 static float gauss_power(const float* co, float dx, float dy)
 {
-    const float q = fmaf(co[0] * dx, dx, (co[2] * dy) * dy);
-    return fmaf(-0.5f, q, -((co[1] * dx) * dy));
+    const float A = -0.5f * co[0], B = -co[1], C = -0.5f * co[2];
+    const float f = fmaf(A, dx, B * dy);
+    return fmaf(dx, f, (C * dy) * dy);
 }
 
 static uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }

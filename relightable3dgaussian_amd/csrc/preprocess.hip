@@ -186,7 +186,9 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     const int RF = 4 * a.rec4;  // floats per record
     if (vis) {
         float* r = s_buf + t * RF;
-        reinterpret_cast<float4*>(r)[0] = rec0;
+        // the blends' staged conic is (-a/2, -b, -c/2): exact (powers of two), so gauss_power is
+        // dx (A dx + B dy) + C dy^2 (r3dg_common.h) and the cull recovers (a, b, c) exactly
+        reinterpret_cast<float4*>(r)[0] = make_float4(-0.5f * rec0.x, -rec0.y, -0.5f * rec0.z, rec0.w);
         reinterpret_cast<float4*>(r)[1] = rec1;
         reinterpret_cast<float4*>(r)[2] = make_float4(col[0], col[1], col[2], depth);
     }

@@ -209,11 +209,18 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));    // packed fp32 pair 
 // FMAs (fmad is on by default; the pattern is the compiler's choice); here one fixed FMA
 // pattern, restated operation for operation by the oracle (oracle/r3dg_oracle.c gauss_power), so
 // every call site -- forward, backward, either instance of an unrolled pair -- and the oracle
-// produce the same bits, and the `power > 0` test resolves identically everywhere.
+// produce the same bits, and the `power > 0` test resolves identically everywhere. `co` is the
+// STAGED conic of the render records, (A, B, C) = (-a/2, -b, -c/2) (exact scalings, written by
+// preprocess_kernel): power = dx (A dx + B dy) + C dy^2, five operations after the two offsets
+// (round 4's pattern on (a, b, c) took seven).
 __device__ __forceinline__ float gauss_power(float4 co, float dx, float dy) {
 #pragma clang fp contract(off)
-    const float q = __builtin_fmaf(co.x * dx, dx, (co.z * dy) * dy);
-    return __builtin_fmaf(-0.5f, q, -((co.y * dx) * dy));
+    const float f = __builtin_fmaf(co.x, dx, co.y * dy);
+    return __builtin_fmaf(dx, f, (co.z * dy) * dy);
+}
+// (a, b, c, opacity) of a staged conic (exact)
+__device__ __forceinline__ float4 unstage_conic(float4 co) {
+    return make_float4(-2.0f * co.x, -co.y, -2.0f * co.z, co.w);
 }
 
 // The blend's exp (forward.cu:477 / backward.cu:527 `exp(power)`, i.e. CUDA expf: <= 2 ulp,
@@ -417,31 +424,17 @@ __device__ __forceinline__ bool rect_culled(float4 co, float mx, float my, float
     return qmin > t;  // false for a NaN / infinite bound: keep
 }
 
-// quadrant_mask's test for one quadrant with top-left pixel (qx, qy): may alpha reach 1/255 there
-// (bit q of quadrant_mask(xy, co, x0, y0, cull) for qx = x0 + (q & 1) * 8, qy = y0 + (q >> 1) * 8).
-__device__ __forceinline__ bool quadrant_live(float2 xy, float4 co, float qx, float qy, int cull) {
+// The exact per-quadrant cull: may alpha = o exp(-Q/2) reach 1/255 anywhere in the 8x8 quadrant with
+// top-left pixel (qx, qy) (rect_culled's margin), so a dropped instance fails the reference's alpha
+// test on every pixel of the quadrant (tests/test_gpu_parity.py: cull on == off bitwise). Takes the
+// render record's staged conic (gauss_power).
+__device__ __forceinline__ bool quadrant_live(float2 xy, float4 staged, float qx, float qy, int cull) {
     if (!cull) return true;
+    const float4 co = unstage_conic(staged);
     if (co.w < 1.0f / 255.0f) return false;
     const float det = co.x * co.z - co.y * co.y;
     if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return true;
     return !rect_culled(co, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f);
-}
-
-// Conservative set of the 8x8 quadrants of tile (x0, y0) in which alpha = o exp(-Q/2) can reach
-// 1/255 (rect_culled's margin), so a dropped instance fails the reference's alpha test on every
-// pixel of the quadrant (tests/test_gpu_parity.py: cull on == off bitwise).
-__device__ __forceinline__ uint32_t quadrant_mask(float2 xy, float4 co, int x0, int y0, int cull) {
-    if (!cull) return 0xFu;
-    if (co.w < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 everywhere
-    const float det = co.x * co.z - co.y * co.y;
-    if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return 0xFu;
-    uint32_t m = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float qx = (float)(x0 + (q & 1) * 8), qy = (float)(y0 + (q >> 1) * 8);
-        if (!rect_culled(co, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f)) m |= 1u << q;
-    }
-    return m;
 }
 
 }  // namespace r3dg

@@ -601,7 +601,14 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     // the default-shader blend sorts its tiles itself (fused, tiles of up to kFusedSortMax instances)
     // only for S <= 12: with more feature channels its registers leave fewer waves to hide the
     // sort's barriers (M1 with S = 21: fused blend 0.78 ms vs 0.49 + 0.10 ms for the separate sort)
-    const bool fuse_sort = !splat_active && S <= 12;
+    // With depth-reading splat shaders the intermediate depth / stencil pass is the first consumer of
+    // the sorted order: every tile is sorted by tile_depth_sort_kernel first (sorting in that pass's
+    // prologue, as the blend does, measured slower: its larger LDS costs the pass more occupancy
+    // than the separate sort, 0.43 + 0.10 -> 0.52 + 0.03 ms per frame at M1 / S = 21, round 5).
+    // Otherwise the blend is the first consumer and sorts tiles of up to kFusedSortMax itself.
+    const bool inter_first = splat_active && inter_pre;
+    const bool fuse_sort = !inter_first && S <= 12;
+    const bool sort_fused = fuse_sort;
     int L = 0;
     BinArgs binning{};
     binning.P = P; binning.grid_x = gx; binning.grid_y = gy; binning.rec4 = record_f4(S); binning.T = T;
@@ -696,7 +703,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         // the default-shader blend sorts the tiles of up to kFusedSortMax instances itself
         R3DG_CHECK_HIP(launch_tile_depth_sort(T, img.ranges, img.tile_order, bin.pairs, bin.point_list,
                                               bin.sort_k1, bin.sort_v1, bin.sort_k2,
-                                              fuse_sort ? kFusedSortMax : 0, st));
+                                              sort_fused ? kFusedSortMax : 0, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
@@ -857,10 +864,10 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         const char* v = getenv("R3DG_BWD");          // the DPP cross-check kernel writes partial rows
         return !(e && e[0] == 'r') && !(v && v[0] == 'd');
     }();
-    // atomic sums: [X part | 6 moments | pad] per Gaussian, rows of 32 floats (128 B) so each
-    // 16-float X segment is one aligned 64-B atomic request
-    // (at least the X part and the 6 moments: XW + 8 floats per row)
-    const int srs_min = 16 * bwd_xblocks(S) + 8;
+    // atomic sums: [X part (f32) | 6 moments (f64) | pad] per Gaussian, rows of 32 floats (128 B) so
+    // each 16-float X segment is one aligned 64-B atomic request and the moments are 8-B aligned
+    // (at least the X part and the 6 double moments: XW + 12 floats per row)
+    const int srs_min = 16 * bwd_xblocks(S) + 12;  // X part + 6 double moment sums
     int SRS = (std::max(RS, srs_min) + 31) & ~31;
     if (const char* e = getenv("R3DG_BWD_SRS")) SRS = std::max(srs_min, atoi(e)) & ~7;  // A/B of the sums' row stride
     const size_t row_bytes = atomic_sums ? 0 : sizeof(float) * (size_t)RS * 4 * L;

@@ -12,8 +12,9 @@
 //      reductions of 13 instances are bf16-split MFMA products (w x [colour, feature, depth grads],
 //      q x pixel moments about the quadrant centre). Default (ATOM): each (instance, wave) row is
 //      expanded about the Gaussian's mean in the lanes and added into the per-Gaussian sums
-//      [P, SRS] with no-return f32 atomics -- the reference's accumulation at 1/64 of its atomics;
-//      the last bits depend on the atomics' arrival order, as the reference's do. w is split into
+//      [P, SRS] with no-return atomics (X part f32, the six moments expanded and summed in f64) --
+//      the reference's accumulation at 1/64 of its atomics; the last bits of the X part depend on
+//      the atomics' arrival order, as the reference's do. w is split into
 //      two bf16 terms (|w - h - m| <= 2^-16 |w|), q into three (exact).
 //      R3DG_BWD_REDUCE=rows (!ATOM): one partial row per (instance, quadrant) at 4 * slot +
 //      quadrant, flagged, summed by
@@ -595,50 +596,56 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         return;
 #endif
         if constexpr (ATOM) {
-            // The moments about the quadrant centre, expanded about the Gaussian's mean once per
-            // row (expand_moments, as row_sum_kernel): D rows go through a 16 x 8 LDS tile in w rows
-            // 0-1 (free once the MFMA operands were read), lane rr = l & 15 expands row rr and writes
-            // it back, then every lane adds its (row, moment) element as before.
+            // The moments about the quadrant centre, expanded about the Gaussian's mean once per row
+            // and summed in double: D rows go through a 16 x 8 float tile in w rows 0-1 (free once
+            // the MFMA operands were read); lane rr = l & 15 expands row rr in double (expand_moments'
+            // formula) into a 16 x 6 double tile in w rows 2-5, and every lane adds its (row, moment)
+            // element with an f64 atomic into the per-Gaussian moment sums. A needle's expanded terms
+            // (|mean - pixel| ~ 1e3 px) are ~1e3-1e6 times the sums they cancel to: summed in f32 in
+            // arrival order, one Gaussian's dL/dmean2D came out 2370x past its conditioning bound
+            // (test_cull_exact_needles; profiles/r05/README.md).
             float* const yt = wq;
             auto yoff = [](int row) { return (row >> 3) * WQS + (row & 7) * 8; };
+            auto doff = [](int row) { return (2 + (row >> 2)) * WQS + (row & 3) * 16; };  // 8-B aligned
             if (nch < 6) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) yt[yoff((l >> 4) * 4 + i) + nch] = accY[i];
             }
             wave_lds_sync();
-            {
-                const int rr = l & 15;
-                const float2* yr = reinterpret_cast<const float2*>(yt + yoff(rr));
+            if (l < 16) {
+                const float2* yr = reinterpret_cast<const float2*>(yt + yoff(l));
                 const float2 m01 = yr[0], m23 = yr[1], m45 = yr[2];
-                const float2 mxy = *reinterpret_cast<const float2*>(wq + rr * WQS + 64);
-                const float sm[6] = {m01.x, m01.y, m23.x, m23.y, m45.x, m45.y};
-                float e[6];
-                expand_moments(sm, mxy.x - qcx, mxy.y - qcy, e);
-                if (l < 16) {
-                    float2* yw = reinterpret_cast<float2*>(yt + yoff(rr));
-                    yw[0] = make_float2(e[0], e[1]);
-                    yw[1] = make_float2(e[2], e[3]);
-                    yw[2] = make_float2(e[4], e[5]);
-                }
+                const float2 mxy = *reinterpret_cast<const float2*>(wq + l * WQS + 64);
+                const double s0 = m01.x, s1 = m01.y, s2 = m23.x, s3 = m23.y, s4 = m45.x, s5 = m45.y;
+                const double dx0 = (double)mxy.x - (double)qcx, dy0 = (double)mxy.y - (double)qcy;
+                double* yw = reinterpret_cast<double*>(wq + doff(l));
+                yw[0] = s0;
+                yw[1] = dx0 * s0 - s1;
+                yw[2] = dy0 * s0 - s2;
+                yw[3] = dx0 * (dx0 * s0 - 2.0 * s1) + s3;
+                yw[4] = dx0 * (dy0 * s0 - s2) - dy0 * s1 + s4;
+                yw[5] = dy0 * (dy0 * s0 - 2.0 * s2) + s5;
             }
             wave_lds_sync();
             // the four expanded elements of this lane, read together (the compiler would otherwise
             // sink each read into its atomic's masked branch: four dependent LDS round trips)
-            float ev[4];
+            double ev[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) ev[i] = yt[yoff((l >> 4) * 4 + i) + (nch < 6 ? nch : 0)];
+            for (int i = 0; i < 4; ++i)
+                ev[i] = reinterpret_cast<const double*>(wq + doff((l >> 4) * 4 + i))[nch < 6 ? nch : 0];
             asm volatile("" ::"v"(ev[0]), "v"(ev[1]), "v"(ev[2]), "v"(ev[3]));
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int row = (l >> 4) * 4 + i;
-                // (only the two atomics under lane masks; adding 0 from the masked lanes instead
+                // (only the atomics under lane masks; adding 0 from the masked lanes instead
                 // measured 23x slower: rows past the group all name one Gaussian and contend)
                 const bool ok = row < r;
                 float* dst = lane_sums + (uint64_t)rid[i] * srs;
 #pragma unroll
                 for (int xb = 0; xb < NXB; ++xb)
                     if (ok && xb * 16 + nch < 4 + S) R3DG_FLUSH_ADD(dst + xb * 16, accX[xb][i]);
-                if (ok && nch < 6) R3DG_FLUSH_ADD(dst + XW, ev[i]);
+                double* mom = reinterpret_cast<double*>(a.sums + (uint64_t)rid[i] * srs + XW);
+                if (ok && nch < 6) R3DG_FLUSH_ADD(mom + nch, ev[i]);
             }
             wave_lds_sync();
             return;
@@ -1323,24 +1330,33 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     // sum row -> the kRow layout gather_gaussian reads
     float s[NR];
     if (g < a.g_end) {
-        const float4* src = reinterpret_cast<const float4*>(a.sums + (size_t)g * (a.sums_moments ? a.SRS : a.RS));
+        const float* row = a.sums + (size_t)g * (a.sums_moments ? a.SRS : a.RS);
+        const float4* src = reinterpret_cast<const float4*>(row);
         float x[XW + 8];
 #pragma unroll
-        for (int q = 0; q < XW / 4 + 2; ++q) {
+        for (int q = 0; q < XW / 4; ++q) {
             const float4 v = src[q];
             x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
         }
         if (a.sums_moments) {
-            // the atomic flush summed the moments about the mean: expand them as row_sum_kernel does
-            const float S0 = x[XW], Sdx = x[XW + 1], Sdy = x[XW + 2], Sdxdx = x[XW + 3], Sdxdy = x[XW + 4],
-                        Sdydy = x[XW + 5];
+            // the atomic flush summed the moments about the mean in double (render_bwd_glds_kernel):
+            // dL/dmean2D, dL/dconic and dL/dopacity from them in double, rounded once
+            const double2* md = reinterpret_cast<const double2*>(row + XW);
+            const double2 m0 = md[0], m1 = md[1], m2 = md[2];
             const float4 co = a.conic_opacity[g];
-            x[XW + 0] = -0.5f * a.W * co.w * (co.x * Sdx + co.y * Sdy);
-            x[XW + 1] = -0.5f * a.H * co.w * (co.z * Sdy + co.y * Sdx);
-            x[XW + 2] = -0.5f * co.w * Sdxdx;
-            x[XW + 3] = -0.5f * co.w * Sdxdy;
-            x[XW + 4] = -0.5f * co.w * Sdydy;
-            x[XW + 5] = S0;
+            const double o = -0.5 * (double)co.w;
+            x[XW + 0] = (float)(o * a.W * ((double)co.x * m0.y + (double)co.y * m1.x));
+            x[XW + 1] = (float)(o * a.H * ((double)co.z * m1.x + (double)co.y * m0.y));
+            x[XW + 2] = (float)(o * m1.y);
+            x[XW + 3] = (float)(o * m2.x);
+            x[XW + 4] = (float)(o * m2.y);
+            x[XW + 5] = (float)m0.x;
+        } else {
+#pragma unroll
+            for (int q = XW / 4; q < XW / 4 + 2; ++q) {
+                const float4 v = src[q];
+                x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+            }
         }
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) s[kRowColor + ch] = x[ch];

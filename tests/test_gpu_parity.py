@@ -157,7 +157,7 @@ def _cull_on_off(hip_ext, scene, cam, S=11, seed=1, atomic_keys=None):
     for k in ga:
         np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
     assert_hip_runs_agree("cull on/off atomic", ga_atomic, gb_atomic, atomic_keys)
-    return a, (ga_atomic, gb_atomic), (dc, do, dd, df)
+    return a, (ga_atomic, gb_atomic, ga), (dc, do, dd, df)
 
 
 @pytest.mark.timeout(400)
@@ -172,7 +172,7 @@ def test_cull_exact_needles(hip_ext):
     cam = synthetic.m1_camera()
     scene = synthetic.needle_scene(300, S=11, seed=0, cam=cam)
     well = ["dL_dcolors", "dL_dopacity", "dL_dfeatures"]
-    h, (gh, gh_off), (dc, do, dd, df) = _cull_on_off(hip_ext, scene, cam, atomic_keys=well)
+    h, (gh, gh_off, g_rows), (dc, do, dd, df) = _cull_on_off(hip_ext, scene, cam, atomic_keys=well)
     o = _oracle_fwd(scene, cam, 11)
     assert o["num_rendered"] > 1_000_000 and int(o["n_contrib"].max()) > 100
     _check_forward(h, o, 11)
@@ -180,10 +180,13 @@ def test_cull_exact_needles(hip_ext):
     grad_check("needles", gh, go, well)
     # the default atomic flush, cull on AND off, each against the oracle at the conditioning bounds
     # below (cull on / off with the deterministic rows reduction are bitwise equal, _cull_on_off)
-    # the atomic flush's summation order is one more perturbation of these sums: the spread
-    # between the two atomic runs (identical visits, different arrival orders) joins the ulp spread
-    order = {k: np.abs(gh[k].astype(np.float64) - gh_off[k]).reshape(gh[k].shape[0], -1).max(1)
-             for k in ["dL_dmeans3D", "dL_dcov3D", "dL_dscales", "dL_drotations"]}
+    # the atomic flush's summation order is one more perturbation of these sums: the spread among
+    # three summation orders of the same rows (two atomic runs with different arrival orders and the
+    # rows reduction's fixed order) joins the ulp spread
+    order = {}
+    for k in ["dL_dmeans3D", "dL_dcov3D", "dL_dscales", "dL_drotations"]:
+        runs = [x[k].astype(np.float64).reshape(x[k].shape[0], -1) for x in (gh, gh_off, g_rows)]
+        order[k] = np.max([np.abs(p - q).max(1) for i, p in enumerate(runs) for q in runs[i + 1:]], axis=0)
     _needle_ill_conditioned([gh, gh_off], go, o, dc, do, dd, df, order)
 
 

@@ -338,21 +338,31 @@ def test_shader_validation_is_loud(hip_ext):
 
 
 @pytest.mark.gpu
-def test_partial_shader_sets_match_oracle(hip_ext):
+@pytest.mark.parametrize("S", [21, 11])
+def test_partial_shader_sets_match_oracle(hip_ext, S):
     """Only the inputs an active shader writes get working copies, and the pre-shader intermediate
     pass runs only when a depth-reading splat shader (Crack, CrackNoRecon) is active
-    (rasterizer.hip): with SH CullHalf + default and splat Wireframe / QuantizeLight + default, every
-    output still matches the oracle (which copies everything and always runs the pass)."""
+    (rasterizer.hip); without it, at S <= 12, the shader blend sorts its tiles itself (fused, as the
+    default blend). SH CullHalf + default with splat Wireframe / QuantizeLight + default (S = 21),
+    or Dissolve / Stencil + default (S = 11, no 21-channel feature views): every output still
+    matches the oracle (which copies everything and always runs the pass), and so do the keys and
+    the sort order."""
     scene, cam = shader_scene(P=4000, seed=15)
     tex = golden_textures()
     rng = np.random.default_rng(3)
     sh_ids = rng.choice([oracle.SH_NAMES.index("CullHalf"), oracle.SH_NAMES.index("ShDefault")], scene.P)
-    sp_ids = rng.choice([oracle.SP_WIREFRAME, oracle.SP_QUANTIZELIGHT, oracle.SP_DEFAULT], scene.P)
+    sp_set = [oracle.SP_WIREFRAME, oracle.SP_QUANTIZELIGHT] if S == 21 else [oracle.SP_DISSOLVE, oracle.SP_STENCIL]
+    sp_ids = rng.choice(sp_set + [oracle.SP_DEFAULT], scene.P)
     texm = _gpu_textures(hip_ext, tex)
-    h = hip_forward(hip_ext, scene, cam, time=700.0, texture_manager=texm, sh_manager=_manager(hip_ext, 0, sh_ids),
-                    splat_manager=_manager(hip_ext, 1, sp_ids))
+    h = hip_forward(hip_ext, scene, cam, S=S, time=700.0, texture_manager=texm,
+                    sh_manager=_manager(hip_ext, 0, sh_ids), splat_manager=_manager(hip_ext, 1, sp_ids))
     T = {k: oracle.Texture(v, mode=4) for k, v in tex.items()}
-    o = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features, sh=scene.sh, scales=scene.scales,
-                                 rotations=scene.rotations, sh_shaders=sh_ids, splat_shaders=sp_ids, textures=T,
-                                 error_texture=T["Error"], time=700.0)
+    o = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features[:, :S], sh=scene.sh,
+                                 scales=scene.scales, rotations=scene.rotations, sh_shaders=sh_ids,
+                                 splat_shaders=sp_ids, textures=T, error_texture=T["Error"], time=700.0)
     _check(h, o)
+    import relightable3dgaussian_amd as r
+
+    st = r._C.rasterizer_state(h["geom"], h["binning"], h["image"], scene.P, cam.height, cam.width,
+                               h["num_rendered"])
+    np.testing.assert_array_equal(st[1].cpu().numpy().view(np.uint32), o["point_list"])
