@@ -57,9 +57,13 @@ static size_t scan_temp_size(size_t P) {
     return bytes;
 }
 
-static bool use_tile_order() {
+// the backward's launch order (read per call): default the per-XCD-band longest-first order;
+// R3DG_TILE_ORDER=longest the global longest-first order, =xcd the plain spatial XCD-aware order
+static const uint32_t* bwd_tile_order(const ImageState& is, int T) {
     const char* e = getenv("R3DG_TILE_ORDER");
-    return !(e && e[0] == 'x');  // backward: "xcd" = spatial XCD-aware order; default longest first
+    if (e && e[0] == 'x') return nullptr;
+    if ((e && e[0] == 'l') || T > 40 * 1024) return is.tile_order;  // (no band order past 40 K tiles)
+    return is.band_order;
 }
 
 // Carving works on an integer cursor so the same code computes sizes (base 0) and pointers.
@@ -128,7 +132,8 @@ static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end, bool wi
     s.n_contrib = carve<uint32_t>(p, N);
     const size_t T = (size_t)num_tiles_of(H, W);
     s.ranges = carve<uint2>(p, T);
-    s.tile_order = carve<uint32_t>(p, T);
+    s.tile_order = carve<uint32_t>(p, padded_tile_grid((int)T));
+    s.band_order = carve<uint32_t>(p, padded_tile_grid((int)T));
     s.tile_work = carve<uint32_t>(p, T);
     // the binning's per-workgroup tile counts: last, so the backward's view of the buffer does
     // not depend on whether they live here (r3dg_rasterize_gaussians) or in transient scratch
@@ -669,7 +674,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         // scatter positions run on the device while the host waits for num_rendered and allocates
         {
             ProfScope ps(R3DG_PROF_SORT, st, true);
-            R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, st));
+            R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, img.band_order, st));
             R3DG_CHECK_LAUNCH(s->debug, st);
         }
         R3DG_CHECK_HIP(hipEventSynchronize(rb->ev));
@@ -681,7 +686,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         L = (int)Lh;
     } else if (T > 0) {  // no Gaussians: every tile range empty
         R3DG_CHECK_HIP(hipMemsetAsync(img.tile_work, 0, sizeof(uint32_t) * (size_t)T, st));
-        R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, st));
+        R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, img.band_order, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 
@@ -910,7 +915,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         ba.dL_dpix_f = gr->dL_dout_feature;
         ba.gflay = make_feature_layout(S, HW, gr->feature_native != 0);
         ba.S = S; ba.W = W; ba.H = H; ba.grid_x = gx; ba.grid_y = gy; ba.num_tiles = T; ba.cull = 1;
-        ba.tile_order = use_tile_order() ? is.tile_order : nullptr;
+        ba.tile_order = bwd_tile_order(is, T);
         if (const char* e = getenv("R3DG_NO_CULL")) ba.cull = (e[0] == '0');
         ba.backward_geometry = backward_geometry;
         ba.RS = RS;
