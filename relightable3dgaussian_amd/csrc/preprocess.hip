@@ -231,8 +231,8 @@ __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* _
 //   4. bin_offsets_kernel: hist[b, t] = first position of workgroup b's instances of tile t;
 //   5. bin_scatter_kernel: every instance takes the next position of its (workgroup, tile) from
 //      an LDS counter and writes (depth bits, Gaussian id) there -- one 8-byte store, and the
-//      depth sort reads its keys coalesced instead of gathering them per instance (also zeroes
-//      the backward's row flags and stores each Gaussian's first slot in its render record).
+//      depth sort reads its keys coalesced instead of gathering them per instance (also stores
+//      each Gaussian's first slot in its render record; zeroes row flags when given them).
 // No global atomics: they execute at the memory side (MI355X_MICROARCH.md "Global float
 // atomics"), one 64-B request per scattered lane -- a first version with one per instance took
 // 0.18 ms per pass at M1. Steps 1-4 need only the scan of tiles touched, so they run while the
@@ -439,19 +439,11 @@ __device__ __forceinline__ uint32_t block_exclusive_scan_1024(uint32_t v, uint32
 // (measured: exact-count buckets, which scatter the tiles of a bucket spatially, slowed the
 // backward by 3 %). Thread t owns the PER tiles [t PER, t PER + PER), held in registers: one round of
 // independent loads (PER = 0: any T, counts re-read).
-//
-// band_order (PER > 0, optional): the backward's launch order -- the same buckets, but per XCD band:
-// workgroup b runs on XCD b % 8 and takes band (b % 8)'s (b / 8)-th longest tile, where band x is the
-// tiles [x per, (x + 1) per) of xcd_tile's spatial split (per = padded tiles / 8). Each XCD's L2 then
-// sees one band of the image (a Gaussian's records and atomic sums stay in one L2) and each XCD
-// still starts with its heaviest tiles. Unfilled slots (short last band) hold T.
 template <int PER>
 __global__ void __launch_bounds__(1024) tile_ranges_kernel(int T, uint32_t* __restrict__ work,
-                                                           uint2* __restrict__ ranges, uint32_t* __restrict__ order,
-                                                           uint32_t* __restrict__ band_order) {
+                                                           uint2* __restrict__ ranges, uint32_t* __restrict__ order) {
     constexpr int NBK = 1024;
     __shared__ uint32_t hist[NBK];
-    __shared__ uint32_t hband[PER > 0 ? 8 * NBK : 1];
     __shared__ uint32_t s_wave[16];
     const int t = threadIdx.x;
     const int per = PER > 0 ? PER : (T + 1023) / 1024;
@@ -508,34 +500,38 @@ __global__ void __launch_bounds__(1024) tile_ranges_kernel(int T, uint32_t* __re
     }
     const int TP = padded_tile_grid(T);
     if (t < TP - T) order[T + t] = (uint32_t)T;  // the padded grid's last workgroups: no tile
-    if constexpr (PER > 0) {
-        if (!band_order) return;  // block-uniform
-        const int per_band = TP >> 3;
-#pragma unroll
-        for (int x = 0; x < 8; ++x) hband[x * NBK + t] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < PER; ++k)
-            if (b0 + k < b1) atomicAdd(&hband[((b0 + k) / per_band) * NBK + bucket(c[k])], 1u);
-        __syncthreads();
-        for (int x = 0; x < 8; ++x) {  // descending bucket order within each band
-            const uint32_t v = hband[x * NBK + NBK - 1 - t];
-            hband[x * NBK + NBK - 1 - t] = block_exclusive_scan_1024(v, s_wave);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int i = b0 + k;
-            if (i < b1) {
-                const int x = i / per_band;
-                band_order[8 * atomicAdd(&hband[x * NBK + bucket(c[k])], 1u) + x] = (uint32_t)i;
-            }
-        }
-        for (int sl = t; sl < TP; sl += 1024) {
-            const int x = sl & 7, rank = sl >> 3;
-            if (rank >= min(per_band, max(0, T - x * per_band))) band_order[sl] = (uint32_t)T;
-        }
+}
+
+// The backward's launch order (band_order): the same count buckets, sorted within each of
+// xcd_tile's eight spatial bands -- slot 8k + x holds band x's k-th longest tile (workgroup b runs on
+// XCD b % 8), band x being the tiles [x per, (x + 1) per), per = padded tiles / 8. Each XCD's L2 then
+// sees one band of the image (a Gaussian's records and atomic sums stay in one L2) and each XCD
+// still starts with its heaviest tiles. One workgroup per band; slots past a short band hold T.
+__global__ void __launch_bounds__(1024) band_order_kernel(int T, const uint2* __restrict__ ranges,
+                                                          uint32_t* __restrict__ band_order) {
+    constexpr int NBK = 1024;
+    __shared__ uint32_t hist[NBK];
+    __shared__ uint32_t s_wave[16];
+    const int t = threadIdx.x, x = blockIdx.x;
+    const int per = padded_tile_grid(T) >> 3;
+    const int i0 = x * per, i1 = min(i0 + per, T);
+    auto bucket = [](uint32_t c) { return (int)min(c >> 2, (uint32_t)(NBK - 1)); };
+    hist[t] = 0;
+    __syncthreads();
+    for (int i = i0 + t; i < i1; i += 1024) {
+        const uint2 r = ranges[i];
+        atomicAdd(&hist[bucket(r.y - r.x)], 1u);
     }
+    __syncthreads();
+    const uint32_t v = hist[NBK - 1 - t];  // descending bucket order
+    const uint32_t ex = block_exclusive_scan_1024(v, s_wave);
+    hist[NBK - 1 - t] = ex;
+    __syncthreads();
+    for (int i = i0 + t; i < i1; i += 1024) {
+        const uint2 r = ranges[i];
+        band_order[8 * atomicAdd(&hist[bucket(r.y - r.x)], 1u) + x] = (uint32_t)i;
+    }
+    for (int k = max(i1 - i0, 0) + t; k < per; k += 1024) band_order[8 * k + x] = (uint32_t)T;
 }
 
 hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, uint32_t* band_order, hipStream_t st) {
@@ -551,14 +547,13 @@ hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, 
         }
     }
     if (a.T <= 8 * 1024)
-        hipLaunchKernelGGL(tile_ranges_kernel<8>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order,
-                           band_order);
+        hipLaunchKernelGGL(tile_ranges_kernel<8>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
     else if (a.T <= 40 * 1024)
-        hipLaunchKernelGGL(tile_ranges_kernel<40>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order,
-                           band_order);
+        hipLaunchKernelGGL(tile_ranges_kernel<40>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
     else
-        hipLaunchKernelGGL(tile_ranges_kernel<0>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order,
-                           nullptr);  // (no band order: the backward takes the global order)
+        hipLaunchKernelGGL(tile_ranges_kernel<0>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
+    if (band_order && order)
+        hipLaunchKernelGGL(band_order_kernel, dim3(8), dim3(1024), 0, st, a.T, ranges, band_order);
     if (a.P > 0 && a.hist) hipLaunchKernelGGL(bin_offsets_kernel, dim3((a.T + 63) / 64), dim3(1024), 0, st, a);
     return hipGetLastError();
 }

@@ -59,10 +59,10 @@ static size_t scan_temp_size(size_t P) {
 
 // the backward's launch order (read per call): default the per-XCD-band longest-first order;
 // R3DG_TILE_ORDER=longest the global longest-first order, =xcd the plain spatial XCD-aware order
-static const uint32_t* bwd_tile_order(const ImageState& is, int T) {
+static const uint32_t* bwd_tile_order(const ImageState& is) {
     const char* e = getenv("R3DG_TILE_ORDER");
     if (e && e[0] == 'x') return nullptr;
-    if ((e && e[0] == 'l') || T > 40 * 1024) return is.tile_order;  // (no band order past 40 K tiles)
+    if (e && e[0] == 'l') return is.tile_order;
     return is.band_order;
 }
 
@@ -697,12 +697,12 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     }
     BinningState bin = binning_state_from(bin_base, (size_t)L);
     if (L > 0) {
-        // every instance to its tile's next position (also zeroes the backward's row flags and
-        // records each Gaussian's first slot), then every tile by (depth bits, Gaussian id): the
+        // every instance to its tile's next position (also records each Gaussian's first slot),
+        // then every tile by (depth bits, Gaussian id): the
         // reference's 45-bit stable sort of (tile << 32 | depth bits) (rasterizer_impl.cu:366-374)
         ProfScope ps(R3DG_PROF_SORT, st, true);
         binning.pairs = bin.pairs;
-        binning.flags = bin.flags;
+        binning.flags = nullptr;  // the rows reduction zeroes its flags itself (backward)
         R3DG_CHECK_HIP(launch_bin_scatter(binning, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
         // the default-shader blend sorts the tiles of up to kFusedSortMax instances itself
@@ -855,8 +855,9 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     const int* radii = radii_in ? radii_in : gs.internal_radii;
     const int RS = part_row_stride(S);
     // scratch: partial rows [4L, RS] (one per instance and quadrant, written sparsely) and the
-    // per-Gaussian sums [P, RS]; the rows' presence flags live in the binning state, zeroed by the
-    // forward's duplicate pass (a row's presence depends on the forward state only)
+    // per-Gaussian sums [P, RS]; the rows' presence flags live in the binning state, zeroed here
+    // (rows reduction only: the default atomic flush has no flags, so the forward's scatter no
+    // longer writes the 4L bytes)
     // the backward blend addresses partial rows with 32-bit offsets in float4 units
     R3DG_REQUIRE((size_t)RS * (size_t)L < (1ull << 32), "rasterize_gaussians_backward: too many tile instances");
     // The second stage of the per-instance reduction (backward.cu:552-611 accumulates per pixel with
@@ -889,6 +890,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         R3DG_CHECK_HIP(hipMemsetAsync(sums, 0, sum_bytes, st));
     }
     uint8_t* flags = reinterpret_cast<uint8_t*>(bs.flags);
+    if (!atomic_sums && L > 0) R3DG_CHECK_HIP(hipMemsetAsync(flags, 0, sizeof(uint32_t) * (size_t)L, st));
     if (L > 0) {
         RenderBwdArgs ba{};
         ba.records = gs.records;
@@ -915,7 +917,7 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         ba.dL_dpix_f = gr->dL_dout_feature;
         ba.gflay = make_feature_layout(S, HW, gr->feature_native != 0);
         ba.S = S; ba.W = W; ba.H = H; ba.grid_x = gx; ba.grid_y = gy; ba.num_tiles = T; ba.cull = 1;
-        ba.tile_order = bwd_tile_order(is, T);
+        ba.tile_order = bwd_tile_order(is);
         if (const char* e = getenv("R3DG_NO_CULL")) ba.cull = (e[0] == '0');
         ba.backward_geometry = backward_geometry;
         ba.RS = RS;
