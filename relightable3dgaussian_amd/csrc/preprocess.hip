@@ -502,39 +502,7 @@ __global__ void __launch_bounds__(1024) tile_ranges_kernel(int T, uint32_t* __re
     if (t < TP - T) order[T + t] = (uint32_t)T;  // the padded grid's last workgroups: no tile
 }
 
-// The backward's launch order (band_order): the same count buckets, sorted within each of
-// xcd_tile's eight spatial bands -- slot 8k + x holds band x's k-th longest tile (workgroup b runs on
-// XCD b % 8), band x being the tiles [x per, (x + 1) per), per = padded tiles / 8. Each XCD's L2 then
-// sees one band of the image (a Gaussian's records and atomic sums stay in one L2) and each XCD
-// still starts with its heaviest tiles. One workgroup per band; slots past a short band hold T.
-__global__ void __launch_bounds__(1024) band_order_kernel(int T, const uint2* __restrict__ ranges,
-                                                          uint32_t* __restrict__ band_order) {
-    constexpr int NBK = 1024;
-    __shared__ uint32_t hist[NBK];
-    __shared__ uint32_t s_wave[16];
-    const int t = threadIdx.x, x = blockIdx.x;
-    const int per = padded_tile_grid(T) >> 3;
-    const int i0 = x * per, i1 = min(i0 + per, T);
-    auto bucket = [](uint32_t c) { return (int)min(c >> 2, (uint32_t)(NBK - 1)); };
-    hist[t] = 0;
-    __syncthreads();
-    for (int i = i0 + t; i < i1; i += 1024) {
-        const uint2 r = ranges[i];
-        atomicAdd(&hist[bucket(r.y - r.x)], 1u);
-    }
-    __syncthreads();
-    const uint32_t v = hist[NBK - 1 - t];  // descending bucket order
-    const uint32_t ex = block_exclusive_scan_1024(v, s_wave);
-    hist[NBK - 1 - t] = ex;
-    __syncthreads();
-    for (int i = i0 + t; i < i1; i += 1024) {
-        const uint2 r = ranges[i];
-        band_order[8 * atomicAdd(&hist[bucket(r.y - r.x)], 1u) + x] = (uint32_t)i;
-    }
-    for (int k = max(i1 - i0, 0) + t; k < per; k += 1024) band_order[8 * k + x] = (uint32_t)T;
-}
-
-hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, uint32_t* band_order, hipStream_t st) {
+hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st) {
     if (a.T <= 0) return hipSuccess;
     if (a.P > 0) {
         if (a.hist) {
@@ -552,8 +520,6 @@ hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, 
         hipLaunchKernelGGL(tile_ranges_kernel<40>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
     else
         hipLaunchKernelGGL(tile_ranges_kernel<0>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
-    if (band_order && order)
-        hipLaunchKernelGGL(band_order_kernel, dim3(8), dim3(1024), 0, st, a.T, ranges, band_order);
     if (a.P > 0 && a.hist) hipLaunchKernelGGL(bin_offsets_kernel, dim3((a.T + 63) / 64), dim3(1024), 0, st, a);
     return hipGetLastError();
 }

@@ -80,8 +80,7 @@ struct ImageState {
     float* final_T;     // [H*W]
     uint32_t* n_contrib;// [H*W]
     uint2* ranges;      // [tiles]
-    uint32_t* tile_order;        // [padded tiles] tiles by descending instance count (depth-sort launch order)
-    uint32_t* band_order;        // [padded tiles] per XCD band, by descending count (backward launch order)
+    uint32_t* tile_order;        // [padded tiles] tiles by descending instance count (blend launch order)
     uint32_t* tile_work;         // [tiles] binning: instance count per tile, then its first position
     uint32_t* bin_hist;          // [bin_blocks_max(tiles), tiles] binning: per-workgroup counts / positions
 };

@@ -211,7 +211,7 @@ struct IntermediateArgs {
 __global__ void preprocess_kernel(PreprocessArgs a);
 __global__ void mark_visible_kernel(int P, const float* means3D, const float* view, uint8_t* present);
 // counts, tile ranges, the longest-first tile order and every workgroup's scatter positions
-hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, uint32_t* band_order, hipStream_t st);
+hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st);
 hipError_t launch_bin_scatter(const BinArgs& a, hipStream_t st);
 // sorts the tiles longer than min_n instances (the forward sorts the others when fused)
 hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint2* pairs,
@@ -276,9 +276,9 @@ __device__ __forceinline__ int xcd_tile(int b, int grid) {
     return (b & 7) * per + (b >> 3);
 }
 // Tile of workgroup b: from a launch order when one is given (padded_tile_grid entries, num_tiles
-// marking a slot without a tile): the longest tiles first, globally or per XCD band (workgroups are
-// dispatched in index order, so the heaviest tiles start first and the tail is made of short
-// tiles; tile_ranges_kernel), else the XCD-aware spatial order.
+// marking a slot without a tile): the longest tiles first (workgroups are dispatched in index
+// order, so the heaviest tiles start first and the tail is made of short tiles;
+// tile_ranges_kernel), else the XCD-aware spatial order.
 __device__ __forceinline__ int block_tile(const uint32_t* order, int num_tiles) {
     const int b = blockIdx.x;
     if (order) return (int)order[b];

@@ -57,13 +57,11 @@ static size_t scan_temp_size(size_t P) {
     return bytes;
 }
 
-// the backward's launch order (read per call): default the per-XCD-band longest-first order;
-// R3DG_TILE_ORDER=longest the global longest-first order, =xcd the plain spatial XCD-aware order
+// the backward's launch order (read per call): longest tiles first; R3DG_TILE_ORDER=xcd the
+// XCD-aware spatial order (per-XCD-band orders measured and dropped)
 static const uint32_t* bwd_tile_order(const ImageState& is) {
     const char* e = getenv("R3DG_TILE_ORDER");
-    if (e && e[0] == 'x') return nullptr;
-    if (e && e[0] == 'l') return is.tile_order;
-    return is.band_order;
+    return (e && e[0] == 'x') ? nullptr : is.tile_order;
 }
 
 // Carving works on an integer cursor so the same code computes sizes (base 0) and pointers.
@@ -133,7 +131,6 @@ static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end, bool wi
     const size_t T = (size_t)num_tiles_of(H, W);
     s.ranges = carve<uint2>(p, T);
     s.tile_order = carve<uint32_t>(p, padded_tile_grid((int)T));
-    s.band_order = carve<uint32_t>(p, padded_tile_grid((int)T));
     s.tile_work = carve<uint32_t>(p, T);
     // the binning's per-workgroup tile counts: last, so the backward's view of the buffer does
     // not depend on whether they live here (r3dg_rasterize_gaussians) or in transient scratch
@@ -674,7 +671,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         // scatter positions run on the device while the host waits for num_rendered and allocates
         {
             ProfScope ps(R3DG_PROF_SORT, st, true);
-            R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, img.band_order, st));
+            R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, st));
             R3DG_CHECK_LAUNCH(s->debug, st);
         }
         R3DG_CHECK_HIP(hipEventSynchronize(rb->ev));
@@ -686,7 +683,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         L = (int)Lh;
     } else if (T > 0) {  // no Gaussians: every tile range empty
         R3DG_CHECK_HIP(hipMemsetAsync(img.tile_work, 0, sizeof(uint32_t) * (size_t)T, st));
-        R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, img.band_order, st));
+        R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
 

@@ -328,22 +328,21 @@ def test_backward_deterministic(hip_ext):
 
 @pytest.mark.parametrize("size", [(100, 90), (208, 160)])
 def test_backward_launch_orders(hip_ext, size, monkeypatch):
-    """The backward's tile launch order only schedules: the per-XCD-band longest-first order (default,
-    tile_ranges_kernel band_order), the global longest-first order (R3DG_TILE_ORDER=longest) and the
-    plain spatial XCD order (=xcd) give bitwise the same gradients on the rows reduction. 100 x 90: 42
-    tiles on a 48-workgroup grid (band 7 empty, band 6 short: sentinel slots); 208 x 160: 130 tiles."""
+    """The backward's tile launch order only schedules: longest tiles first (default,
+    tile_ranges_kernel; padded-grid slots past the last tile are empty) and the XCD-aware spatial
+    order (R3DG_TILE_ORDER=xcd) give bitwise the same gradients on the rows reduction. 100 x 90: 42
+    tiles on a 48-workgroup grid; 208 x 160: 130 tiles on 136."""
     W, H = size
     scene, cam = synthetic.small_scene(P=3000, S=11, seed=4, width=W, height=H)
     dc, do, dd, df = upstream_grads(cam.height, cam.width, 11)
     g = {}
     with rows_reduction():
         h = hip_forward(hip_ext, scene, cam, S=11)
-        for order in ("band", "longest", "xcd"):
+        for order in ("longest", "xcd"):
             monkeypatch.setenv("R3DG_TILE_ORDER", order)
             g[order] = hip_backward(hip_ext, h, dc, do, dd, df)
-    for order in ("longest", "xcd"):
-        for k in g["band"]:
-            np.testing.assert_array_equal(g[order][k], g["band"][k], err_msg=f"{order} {k}")
+    for k in g["longest"]:
+        np.testing.assert_array_equal(g["xcd"][k], g["longest"][k], err_msg=k)
 
 
 @pytest.mark.parametrize("reduce", ["rows", "atomic"])
