@@ -285,9 +285,12 @@ def rasterize_forward(cam, means3D, opacity, features, sh=None, degree=3, scales
 
 
 def rasterize_backward(fwd, dL_dcolor, dL_dopacity, dL_ddepth, dL_dfeature, color_hwc=False, feature_native=False,
-                       backward_geometry=True):
+                       backward_geometry=True, acc64=False):
     """rasterize_gaussians_backward (rasterizer_impl.cu:533-639). Grad layouts: colour CHW [3,H,W]
-    (reference) unless color_hwc; features planar [S,H,W] (reference) unless feature_native."""
+    (reference) unless color_hwc; features planar [S,H,W] (reference) unless feature_native.
+    acc64 (test-only accuracy reference, not the reference's arithmetic): the per-pixel mean2D /
+    conic / opacity terms formed in double and summed in double, rounded to f32 once, then the same
+    f32 per-Gaussian backward."""
     L_ = lib()
     i = fwd["_in"]
     cam = i["cam"]
@@ -310,12 +313,20 @@ def rasterize_backward(fwd, dL_dcolor, dL_dopacity, dL_ddepth, dL_dfeature, colo
     dfeat = np.zeros((P, S), F)
     gc, go, gd = _f(dL_dcolor), _f(dL_dopacity), _f(dL_ddepth)
     gf = _f(dL_dfeature) if S else np.zeros(1, F)
+    if acc64:
+        a64 = [np.zeros((P, 3)), np.zeros((P, 4)), np.zeros((P, 1))]
+        L_.oracle_set_render_bwd_acc64(*[a.ctypes.data_as(ctypes.c_void_p) for a in a64])
     L_.oracle_render_backward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(S), _p(fwd["ranges"]),
                               _p(np.ascontiguousarray(fwd["point_list"])), _p(i["bg"]), _p(fwd["means2D"]),
                               _p(fwd["depths"]), _p(fwd["conic_opacity"]), _p(colors), _p(i["features"]),
                               _p(fwd["final_T"]), _p(np.ascontiguousarray(fwd["n_contrib"].reshape(-1))), _p(gc),
                               _p(ca), _p(cm), _p(go), _p(gd), _p(gf), _p(fa), _p(fm), ctypes.c_int(int(backward_geometry)),
                               _p(dmean2D), _p(dconic), _p(dopac), _p(dcol), _p(dfeat))
+    if acc64:
+        L_.oracle_set_render_bwd_acc64(None, None, None)
+        dmean2D[:] = a64[0].astype(F)
+        dconic[:] = a64[1].astype(F)
+        dopac[:] = a64[2].astype(F)
     M = 0 if i["sh"] is None else i["sh"].shape[1]
     dmean3D = np.zeros((P, 3), F)
     dcov = np.zeros((P, 6), F)

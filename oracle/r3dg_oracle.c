@@ -653,6 +653,19 @@ void oracle_surface_xyz_normal(int W, int H, const float* view, float fx, float 
 /* tile blend, backward (backward.cu:401-614). Gradients accumulate sequentially.               */
 /* grad layouts: colour channel c of pixel pix at dcol[ca[c] + pix*cm[c]], same for features.  */
 /* ------------------------------------------------------------------------------------------ */
+/* Test-only accuracy reference (not the reference's arithmetic): when set, the per-pixel mean2D /
+   conic / opacity terms below are formed in double from the same f32 per-pixel values and summed
+   into these double accumulators instead of the f32 outputs -- the sums the reference's f32
+   atomics approximate. tests/test_gpu_parity.py (needles) measures the f32 statement's own error
+   against it. */
+static double *g_acc64_mean2D = NULL, *g_acc64_conic = NULL, *g_acc64_opac = NULL;
+void oracle_set_render_bwd_acc64(double* mean2D, double* conic, double* opac)
+{
+    g_acc64_mean2D = mean2D;
+    g_acc64_conic = conic;
+    g_acc64_opac = opac;
+}
+
 void oracle_render_backward(int W, int H, int S, const uint32_t* ranges, const uint32_t* point_list,
                             const float* bg, const float* means2D, const float* depths, const float* conic_opacity,
                             const float* colors, const float* features, const float* final_Ts,
@@ -721,6 +734,17 @@ void oracle_render_backward(int W, int H, int S, const uint32_t* ranges, const u
                         last_alpha = alpha;
                         dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
                         const float dL_dG = co[3] * dL_dalpha;
+                        if (g_acc64_mean2D) {
+                            const double dG = (double)co[3] * dL_dalpha, gx = (double)G * dx, gy = (double)G * dy;
+                            g_acc64_mean2D[3 * id + 0] += dG * (-gx * co[0] - gy * co[1]) * ddelx_dx;
+                            g_acc64_mean2D[3 * id + 1] += dG * (-gy * co[2] - gx * co[1]) * ddely_dy;
+                            g_acc64_mean2D[3 * id + 2] += (double)gd * dchannel_dcolor;
+                            g_acc64_conic[4 * id + 0] += -0.5 * gx * dx * dG;
+                            g_acc64_conic[4 * id + 1] += -0.5 * gx * dy * dG;
+                            g_acc64_conic[4 * id + 3] += -0.5 * gy * dy * dG;
+                            g_acc64_opac[id] += (double)G * dL_dalpha;
+                            continue;
+                        }
                         const float gdx = G * dx, gdy = G * dy;
                         const float dG_ddelx = -gdx * co[0] - gdy * co[1];
                         const float dG_ddely = -gdy * co[2] - gdx * co[1];

@@ -79,19 +79,13 @@ __device__ __forceinline__ int block_max_last(int wmax, int* s_max_last) {
 }
 
 // One wave's pixel moments of q, sum q * [1, x, y, x^2, xy, y^2] with (x, y) = pixel - quadrant
-// centre, expanded about the Gaussian's mean: with (d0x, d0y) = mean - quadrant centre the pixel's
-// offset from the mean is (d0x - x, d0y - y), so
+// centre, expanded about the Gaussian's mean ("expand_moments"): with (d0x, d0y) = mean - quadrant
+// centre the pixel's offset from the mean is (d0x - x, d0y - y), so
 //   sum q dx = d0x S0 - Sx,  sum q dx^2 = d0x^2 S0 - 2 d0x Sx + Sxx,  sum q dx dy = d0x d0y S0 - d0x Sy
 //   - d0y Sx + Sxy  (and y alike): the partial row's moments (r3dg_kernels.h), what
-// backward.cu:583-611 sums per pixel through dG/ddelx, dG/ddely and the conic terms.
-__device__ __forceinline__ void expand_moments(const float (&s)[6], float d0x, float d0y, float (&e)[6]) {
-    e[0] = s[0];
-    e[1] = d0x * s[0] - s[1];
-    e[2] = d0y * s[0] - s[2];
-    e[3] = d0x * d0x * s[0] - 2.f * d0x * s[1] + s[3];
-    e[4] = d0x * d0y * s[0] - d0x * s[2] - d0y * s[1] + s[4];
-    e[5] = d0y * d0y * s[0] - 2.f * d0y * s[2] + s[5];
-}
+// backward.cu:583-611 sums per pixel through dG/ddelx, dG/ddely and the conic terms. Both
+// reductions (the atomic flush and row_sum_kernel) evaluate and sum it in double: for a mean ~1e3
+// px from its pixels the terms are ~1e6 times the result.
 
 // DPP variant (cross-check of the MFMA default, R3DG_BWD=dpp): the reference's per-channel
 // recurrences (backward.cu:544-579) step by step; every wave reduces its 64 pixels' values of an
@@ -1234,6 +1228,8 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
     const int g = gb + (int)threadIdx.x / LPG, c = (int)threadIdx.x % LPG;
     const bool active = g < a.g_end && c < NXC + 2;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    double dacc[4] = {0.0, 0.0, 0.0, 0.0};  // moment lanes: the expanded moments, in double as the
+                                            // atomic flush's (needle means ~1e3 px off: DESIGN §5)
     uint32_t k0 = 0, n = 0;
     float2 xy = make_float2(0.f, 0.f);
     if (g < a.g_end && a.rows && a.radii[g] > 0) {  // uniform within the group
@@ -1282,34 +1278,40 @@ __global__ void __launch_bounds__(256) row_sum_kernel(GatherBwdArgs a) {
                     const float4 vo = make_float4(dpp_mov<0xB1>(v[i].x), dpp_mov<0xB1>(v[i].y), dpp_mov<0xB1>(v[i].z),
                                                   dpp_mov<0xB1>(v[i].w));
                     const float4 m0 = c == NXC ? v[i] : vo, m1 = c == NXC ? vo : v[i];
-                    const float sm[6] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y};
-                    float e[6];
-                    // an absent row is all zero: its centre (0, 0) multiplies zero moments
-                    expand_moments(sm, xy.x - m1.z, xy.y - m1.w, e);
+                    // expand_moments' formula in double; an absent row is all zero: its centre
+                    // (0, 0) multiplies zero moments
+                    const double s0 = m0.x, s1 = m0.y, s2 = m0.z, s3 = m0.w, s4 = m1.x, s5 = m1.y;
+                    const double dx0 = (double)xy.x - (double)m1.z, dy0 = (double)xy.y - (double)m1.w;
                     if (c == NXC) {
-                        acc.x += e[0]; acc.y += e[1]; acc.z += e[2]; acc.w += e[3];
+                        dacc[0] += s0;
+                        dacc[1] += dx0 * s0 - s1;
+                        dacc[2] += dy0 * s0 - s2;
+                        dacc[3] += dx0 * (dx0 * s0 - 2.0 * s1) + s3;
                     } else {
-                        acc.x += e[4]; acc.y += e[5];
+                        dacc[0] += dx0 * (dy0 * s0 - s2) - dy0 * s1 + s4;
+                        dacc[1] += dy0 * (dy0 * s0 - 2.0 * s2) + s5;
                     }
                 }
             }
         }
     }
     // lane NXC takes the [Sdxdy, Sdydy] sums of lane NXC + 1 (all lanes take part in the shuffle)
-    const float sxy = __shfl_down(acc.x, 1), syy = __shfl_down(acc.y, 1);
+    const double sxy = __shfl_down(dacc[0], 1), syy = __shfl_down(dacc[1], 1);
     if (!active) return;
     float4* dst = reinterpret_cast<float4*>(a.sums + (size_t)g * RS);
     if (c < NXC) {
         dst[c] = acc;
     } else if (c == NXC) {
-        const float S0 = acc.x, Sdx = acc.y, Sdy = acc.z, Sdxdx = acc.w, Sdxdy = sxy, Sdydy = syy;
+        const double S0 = dacc[0], Sdx = dacc[1], Sdy = dacc[2], Sdxdx = dacc[3], Sdxdy = sxy, Sdydy = syy;
         const float4 co = a.conic_opacity[g];
         // dL/dmean2D = -0.5 (W, H) o (o * conic . (Sdx, Sdy)), dL/dconic = -0.5 o (Sdxdx, Sdxdy,
-        // Sdydy), dL/dopacity = S0 (backward.cu:583-611)
-        dst[NXC] = make_float4(-0.5f * a.W * co.w * (co.x * Sdx + co.y * Sdy),
-                               -0.5f * a.H * co.w * (co.z * Sdy + co.y * Sdx), -0.5f * co.w * Sdxdx,
-                               -0.5f * co.w * Sdxdy);
-        dst[NXC + 1] = make_float4(-0.5f * co.w * Sdydy, S0, 0.f, 0.f);
+        // Sdydy), dL/dopacity = S0 (backward.cu:583-611), in double and rounded once (as the gather
+        // does from the atomic sums)
+        const double o = -0.5 * (double)co.w;
+        dst[NXC] = make_float4((float)(o * a.W * ((double)co.x * Sdx + (double)co.y * Sdy)),
+                               (float)(o * a.H * ((double)co.z * Sdy + (double)co.y * Sdx)), (float)(o * Sdxdx),
+                               (float)(o * Sdxdy));
+        dst[NXC + 1] = make_float4((float)(o * Sdydy), (float)S0, 0.f, 0.f);
     }
 }
 
