@@ -169,6 +169,12 @@ __device__ __forceinline__ int lane_id() { return __lane_id(); }
 // (the per-Gaussian kernels' SH staging; one dword per access kept 8 loads in flight). put(f, v) /
 // get(f) map element f to its LDS slot.
 constexpr int kCopyU = 6;
+// floor(f / d) by one multiply-high, m = fastdiv_magic(d) = ceil(2^32 / d): exact while f * d < 2^32
+// (the SH staging: f < 256 * d, d = 3 M < 4096). The copies below map every element through such a
+// quotient; a plain `/` by a runtime divisor is a ~15-instruction sequence per element (round 5:
+// half the VALU of the gather and preprocess kernels).
+__host__ __device__ inline uint32_t fastdiv_magic(uint32_t d) { return d > 1 ? 0xFFFFFFFFu / d + 1u : 0u; }
+__device__ __forceinline__ int fastdiv(int f, uint32_t m) { return m ? (int)__umulhi((uint32_t)f, m) : f; }
 template <int BT, class F>
 __device__ __forceinline__ void block_load4(const float* __restrict__ src, int n, int t, F&& put) {
     const int n4 = (reinterpret_cast<uintptr_t>(src) & 15u) ? 0 : n >> 2;  // unaligned: dword copies

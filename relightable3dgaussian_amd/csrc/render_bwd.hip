@@ -1177,8 +1177,9 @@ __global__ void __launch_bounds__(kShViewsBlock) sh_grad_views_kernel(int g0, in
     __syncthreads();
     const int M3 = 3 * M, ng = min(kShViewsBlock, n - ib);
     float* o = dsh + (size_t)(g0 + ib) * M3;
+    const uint32_t m3 = fastdiv_magic((uint32_t)M3);
     for (int f = t; f < ng * M3; f += kShViewsBlock) {
-        const int gg = f / M3;
+        const int gg = fastdiv(f, m3);
         o[f] = s_out[gg * SHS + (f - gg * M3)];
     }
 }
@@ -1380,10 +1381,11 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     const int M3 = 3 * a.M;
     const int ng = min(256, a.g_end - g0);
     float* shl = s_buf + t * SHS;
+    const uint32_t m3 = fastdiv_magic((uint32_t)M3);
     if (a.sh && a.dL_dsh) {
         const float* src = a.sh + (size_t)g0 * M3;
         block_load4<256>(src, ng * M3, t, [&](int f, float v) {
-            const int gg = f / M3;
+            const int gg = fastdiv(f, m3);
             s_buf[gg * SHS + (f - gg * M3)] = v;
         });
     }
@@ -1393,7 +1395,7 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
     if (a.dL_dsh) {
         float* dst = a.dL_dsh + (size_t)g0 * M3;
         block_store4<256>(dst, ng * M3, t, [&](int f) {
-            const int gg = f / M3;
+            const int gg = fastdiv(f, m3);
             return s_buf[gg * SHS + (f - gg * M3)];
         });
     }
