@@ -509,11 +509,12 @@ def _brdf_tensors(inp):
 
 
 
-@pytest.mark.parametrize("size", [(3200, 1800), (4200, 2400)])
+@pytest.mark.parametrize("size", [(3200, 1800), (4200, 2400), (7680, 4320)])
 def test_binning_large_frames(hip_ext, size):
-    """Binning above 12288 tiles (3200x1800: 22600 tiles, LDS counters beyond 64 KiB per workgroup)
-    and above kBinMaxTiles (4200x2400: 39450 tiles, the global-atomic fallback): keys, point list
-    and ranges bit-exact vs the oracle."""
+    """Binning above 12288 tiles (3200x1800: 22600 tiles, LDS counters beyond 64 KiB per workgroup),
+    above kBinMaxTiles (4200x2400: 39450 tiles, the global-atomic fallback) and above 40960 tiles
+    (7680x4320: 129600 tiles, tile_ranges_kernel's re-reading PER = 0 path): keys, point list and
+    ranges bit-exact vs the oracle."""
     cam = synthetic.m1_camera(*size)
     scene = synthetic.m1_scene(P=150_000, S=3, seed=5, cam=cam)
     h = hip_forward(hip_ext, scene, cam, S=3)
