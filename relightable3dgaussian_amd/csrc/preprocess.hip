@@ -171,9 +171,10 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
         for (int i = idx; i < a.num_tiles; i += (int)(gridDim.x * 256)) a.tile_count[i] = 0u;
     if (use_sh) {
         const float* src = a.sh + (size_t)g0 * M3;
-        const uint32_t m3 = fastdiv_magic((uint32_t)M3);
+        // (a plain division here: the multiply-high of gather_bwd_kernel measured 2-5 % slower in
+        // this kernel)
         block_load4<256>(src, ng * M3, t, [&](int f, float v) {
-            const int gg = fastdiv(f, m3);
+            const int gg = f / M3;
             s_buf[gg * SHS + (f - gg * M3)] = v;
         });
     }
