@@ -60,8 +60,16 @@ struct BinArgs {
 constexpr int kBinThreads = 1024;                  // binning workgroup (one per CU)
 constexpr int kBinSub = 1024;                      // Gaussians staged in LDS at a time
 constexpr int kBinMaxTiles = (163840 - 16 * kBinSub) / 4;  // LDS counters per workgroup (160 KiB)
-// binning workgroups for T tiles: the [nblk, T] count matrix stays <= 8 MiB
-inline int bin_blocks_max(int T) { return T > kBinMaxTiles ? 0 : std::max(1, std::min(256, (1 << 21) / std::max(T, 1))); }
+// binning workgroups for T tiles: the [nblk, T] count matrix stays <= 4 * R3DG_BIN_MATRIX entries
+#ifndef R3DG_BIN_BLOCKS_MAX
+#define R3DG_BIN_BLOCKS_MAX 256
+#endif
+#ifndef R3DG_BIN_MATRIX
+#define R3DG_BIN_MATRIX (1 << 21)
+#endif
+inline int bin_blocks_max(int T) {
+    return T > kBinMaxTiles ? 0 : std::max(1, std::min(R3DG_BIN_BLOCKS_MAX, R3DG_BIN_MATRIX / std::max(T, 1)));
+}
 
 struct RenderFwdArgs {
     const float4* records;     // render records (record_f4), used by the default-shader kernel
