@@ -246,7 +246,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // by LDS and VGPRs together; the LDS allocation is rounded up in 2 KiB steps.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 #ifndef R3DG_BWD_WAVES
-#define R3DG_BWD_WAVES 4  // waves per SIMD the register allocation targets (SMAX <= 12)
+#define R3DG_BWD_WAVES 3  // waves per SIMD the register allocation targets (SMAX <= 12). The kernel
+                          // takes 125 VGPRs either way and runs 4 waves per SIMD (LDS: 4 blocks per
+                          // CU); the target of 3 only changes the scheduler's latency / pressure
+                          // trade-off: render_bwd -0.4 % at M1 (4 pairs), -0.8 % at C3, round 5
 #endif
 
 // w|q image: row r (0..15 w, 16..31 q) of 64 pixels, padded stride WQS = 66 floats; pixel c of
