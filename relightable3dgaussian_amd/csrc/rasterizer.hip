@@ -787,7 +787,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         xa.W = W; xa.H = H; xa.view = s->viewmatrix; xa.focal_x = focal_x; xa.focal_y = focal_y;
         xa.cx = s->cx; xa.cy = s->cy; xa.opacity = out->opacity; xa.depth = out->depth;
         xa.normal = out->normal; xa.xyz = out->surface_xyz;
-        hipLaunchKernelGGL(xyz_normal_kernel, dim3(gx, gy), dim3(256), 0, st, xa);
+        hipLaunchKernelGGL(xyz_normal_kernel, dim3(gx, (gy + R3DG_XYZ_R - 1) / R3DG_XYZ_R), dim3(256), 0, st, xa);
         R3DG_CHECK_LAUNCH(s->debug, st);
     } else {
         if (out->normal) R3DG_CHECK_HIP(hipMemsetAsync(out->normal, 0, sizeof(float) * 3 * (size_t)H * W, st));

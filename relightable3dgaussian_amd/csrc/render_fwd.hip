@@ -467,66 +467,74 @@ __device__ __forceinline__ float3 surface_point(const XyzNormalArgs& a, int x, i
     return make_float3(((float)x - a.cx) / a.focal_x * d, ((float)y - a.cy) / a.focal_y * d, d);
 }
 
+// One workgroup per 16 x (16 XYZ_R) pixels (XYZ_R tile rows: the halo and the launch's latency
+// amortised over more pixels); thread t handles pixel column t & 15 of rows t >> 4, + 16, ...
+#ifndef R3DG_XYZ_R
+#define R3DG_XYZ_R 4
+#endif
 __global__ void __launch_bounds__(256) xyz_normal_kernel(XyzNormalArgs a) {
-    // the block's 18x18 neighbourhood (edge-clamped) of surface points, each evaluated once into
-    // LDS instead of nine times per pixel
-    __shared__ float sp[3][18 * 18];
-    const int bx = blockIdx.x * 16, by = blockIdx.y * 16;
-    for (int k = threadIdx.x; k < 18 * 18; k += 256) {
-        const int hx = min(max(bx + k % 18 - 1, 0), a.W - 1), hy = min(max(by + k / 18 - 1, 0), a.H - 1);
+    // the block's 18 x (16 R + 2) neighbourhood (edge-clamped) of surface points, each evaluated
+    // once into LDS instead of nine times per pixel
+    constexpr int R = R3DG_XYZ_R, HW_ = 18, HH = 16 * R + 2;
+    __shared__ float sp[3][HW_ * HH];
+    const int bx = blockIdx.x * 16, by = blockIdx.y * 16 * R;
+    for (int k = threadIdx.x; k < HW_ * HH; k += 256) {
+        const int hx = min(max(bx + k % HW_ - 1, 0), a.W - 1), hy = min(max(by + k / HW_ - 1, 0), a.H - 1);
         const float3 q = surface_point(a, hx, hy);
         sp[0][k] = q.x;
         sp[1][k] = q.y;
         sp[2][k] = q.z;
     }
     __syncthreads();
-    const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
-    const int x = bx + lx, y = by + ly;
-    if (x >= a.W || y >= a.H) return;
-    const int pix = y * a.W + x;
-    // neighbour (dx, dy) of this pixel; edge clamping already happened in the halo load, except
-    // that a pixel on the image's last row / column inside the block must clamp to itself
-    const int xm = lx, xc = lx + 1, xp = x == a.W - 1 ? lx + 1 : lx + 2;
-    const int ym = ly, yc = ly + 1, yp = y == a.H - 1 ? ly + 1 : ly + 2;
-    auto P3 = [&](int hx, int hy) {
-        const int k = hy * 18 + hx;
-        return make_float3(sp[0][k], sp[1][k], sp[2][k]);
-    };
-    const float3 c = P3(xc, yc);
-    a.xyz[3 * pix + 0] = c.x;
-    a.xyz[3 * pix + 1] = c.y;
-    a.xyz[3 * pix + 2] = c.z;
-    const float3 p00 = P3(xm, ym), p01 = P3(xc, ym), p02 = P3(xp, ym);
-    const float3 p10 = P3(xm, yc), p12 = P3(xp, yc);
-    const float3 p20 = P3(xm, yp), p21 = P3(xc, yp), p22 = P3(xp, yp);
-    float ga[3], gb[3];
-    const float3 q00 = p00, q01 = p01, q02 = p02, q10 = p10, q12 = p12, q20 = p20, q21 = p21, q22 = p22;
-    const float* f00 = &q00.x; const float* f01 = &q01.x; const float* f02 = &q02.x; const float* f10 = &q10.x;
-    const float* f12 = &q12.x; const float* f20 = &q20.x; const float* f21 = &q21.x; const float* f22 = &q22.x;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        ga[i] = -0.125f * f00[i] + 0.125f * f02[i] - 0.25f * f10[i] + 0.25f * f12[i] - 0.125f * f20[i] +
-                0.125f * f22[i];
-        gb[i] = -0.125f * f00[i] - 0.25f * f01[i] - 0.125f * f02[i] + 0.125f * f20[i] + 0.25f * f21[i] +
-                0.125f * f22[i];
-    }
-    float nx = ga[1] * gb[2] - ga[2] * gb[1];
-    float ny = -ga[0] * gb[2] + ga[2] * gb[0];
-    float nz = ga[0] * gb[1] - ga[1] * gb[0];
-    const float norm = sqrtf(nx * nx + ny * ny + nz * nz);
-    if (norm <= 0.0f) {
-        a.normal[3 * pix + 0] = 0.f;
-        a.normal[3 * pix + 1] = 0.f;
-        a.normal[3 * pix + 2] = 0.f;
-        return;
-    }
-    nx = -nx / norm;
-    ny = -ny / norm;
-    nz = -nz / norm;
     const float* v = a.view;
-    a.normal[3 * pix + 0] = v[0] * nx + v[1] * ny + v[2] * nz;
-    a.normal[3 * pix + 1] = v[4] * nx + v[5] * ny + v[6] * nz;
-    a.normal[3 * pix + 2] = v[8] * nx + v[9] * ny + v[10] * nz;
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+        const int lx = threadIdx.x & 15, ly = (threadIdx.x >> 4) + 16 * rr;
+        const int x = bx + lx, y = by + ly;
+        if (x >= a.W || y >= a.H) continue;
+        const int pix = y * a.W + x;
+        // neighbour (dx, dy) of this pixel; edge clamping already happened in the halo load, except
+        // that a pixel on the image's last row / column inside the block must clamp to itself
+        const int xm = lx, xc = lx + 1, xp = x == a.W - 1 ? lx + 1 : lx + 2;
+        const int ym = ly, yc = ly + 1, yp = y == a.H - 1 ? ly + 1 : ly + 2;
+        auto P3 = [&](int hx, int hy) {
+            const int k = hy * HW_ + hx;
+            return make_float3(sp[0][k], sp[1][k], sp[2][k]);
+        };
+        const float3 c = P3(xc, yc);
+        a.xyz[3 * pix + 0] = c.x;
+        a.xyz[3 * pix + 1] = c.y;
+        a.xyz[3 * pix + 2] = c.z;
+        const float3 p00 = P3(xm, ym), p01 = P3(xc, ym), p02 = P3(xp, ym);
+        const float3 p10 = P3(xm, yc), p12 = P3(xp, yc);
+        const float3 p20 = P3(xm, yp), p21 = P3(xc, yp), p22 = P3(xp, yp);
+        float ga[3], gb[3];
+        const float* f00 = &p00.x; const float* f01 = &p01.x; const float* f02 = &p02.x; const float* f10 = &p10.x;
+        const float* f12 = &p12.x; const float* f20 = &p20.x; const float* f21 = &p21.x; const float* f22 = &p22.x;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            ga[i] = -0.125f * f00[i] + 0.125f * f02[i] - 0.25f * f10[i] + 0.25f * f12[i] - 0.125f * f20[i] +
+                    0.125f * f22[i];
+            gb[i] = -0.125f * f00[i] - 0.25f * f01[i] - 0.125f * f02[i] + 0.125f * f20[i] + 0.25f * f21[i] +
+                    0.125f * f22[i];
+        }
+        float nx = ga[1] * gb[2] - ga[2] * gb[1];
+        float ny = -ga[0] * gb[2] + ga[2] * gb[0];
+        float nz = ga[0] * gb[1] - ga[1] * gb[0];
+        const float norm = sqrtf(nx * nx + ny * ny + nz * nz);
+        if (norm <= 0.0f) {
+            a.normal[3 * pix + 0] = 0.f;
+            a.normal[3 * pix + 1] = 0.f;
+            a.normal[3 * pix + 2] = 0.f;
+            continue;
+        }
+        nx = -nx / norm;
+        ny = -ny / norm;
+        nz = -nz / norm;
+        a.normal[3 * pix + 0] = v[0] * nx + v[1] * ny + v[2] * nz;
+        a.normal[3 * pix + 1] = v[4] * nx + v[5] * ny + v[6] * nz;
+        a.normal[3 * pix + 2] = v[8] * nx + v[9] * ny + v[10] * nz;
+    }
 }
 
 }  // namespace r3dg
