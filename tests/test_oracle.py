@@ -257,6 +257,29 @@ def _fd_loss(cam, scene, up):
             + np.sum(df.astype(f64) * o["feature"].reshape(-1).reshape(S, H, W))), o
 
 
+def test_backward_acc64_variant():
+    """oracle.rasterize_backward(acc64=True) (the needle test's accuracy reference: the per-pixel
+    mean2D / conic / opacity terms formed and summed in double) agrees with the f32 statement on a
+    well-conditioned scene to f32 summation level, leaves the other gradients untouched, and resets
+    (a following f32 call is bitwise the first)."""
+    scene, cam = synthetic.small_scene(P=800, S=3, seed=6, width=64, height=48)
+    o = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features, sh=scene.sh, scales=scene.scales,
+                                 rotations=scene.rotations)
+    rng = np.random.default_rng(4)
+    H, W = cam.height, cam.width
+    up = tuple(rng.normal(size=s).astype(np.float32) for s in [(3, H, W), (H, W), (H, W), (3, H, W)])
+    g = oracle.rasterize_backward(o, *up)
+    g64 = oracle.rasterize_backward(o, *up, acc64=True)
+    g2 = oracle.rasterize_backward(o, *up)
+    for k in g:
+        np.testing.assert_array_equal(g2[k], g[k], err_msg=k)
+    for k in ["dL_dcolors", "dL_dfeatures"]:
+        np.testing.assert_array_equal(g64[k], g[k], err_msg=k)
+    for k in ["dL_dmeans2D", "dL_dopacity", "dL_dmeans3D", "dL_dconic"]:
+        m = float(np.abs(g[k]).max())
+        assert float(np.abs(g64[k] - g[k]).max()) <= 1e-5 * m, k
+
+
 def test_backward_is_gradient_of_forward():
     """Central differences of the oracle forward vs its analytic backward (means3D, opacity,
     scales, rotations, SH DC, features). The forward has measure-zero discontinuities (alpha
