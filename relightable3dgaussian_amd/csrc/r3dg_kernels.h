@@ -242,7 +242,7 @@ __device__ __forceinline__ uint32_t instance_slot(const uint32_t* offsets, float
     return (g == 0 ? 0u : offsets[g - 1]) + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
 }
 #ifndef R3DG_XYZ_R
-#define R3DG_XYZ_R 4  // tile rows per xyz_normal_kernel workgroup (render_fwd.hip; 1 / 2 / 4: 25.7 / 25.0 / 21.7 us at M1)
+#define R3DG_XYZ_R 4  // tile rows per xyz_normal_kernel workgroup (render_fwd.hip; 1 / 2 / 4 / 8: 25.7 / 25.0 / 21.7 / 24.9 us at M1)
 #endif
 __global__ void xyz_normal_kernel(XyzNormalArgs a);
 // RenderIntermediateTextures: packs the per-Gaussian depth / stencil record, then the DMA-staged blend

@@ -62,7 +62,7 @@ def _check_forward(h, o, S):
     np.testing.assert_array_equal(h["stencil"].cpu().numpy(), 0.0)
 
 
-@pytest.mark.parametrize("S", [0, 3, 11, 21, 32])
+@pytest.mark.parametrize("S", [0, 3, 6, 11, 12, 16, 21, 32])  # every SMAX instantiation (S <= 0/4/8/11/12/16/24/32)
 def test_forward_matches_oracle(hip_ext, S):
     scene, cam = synthetic.small_scene(P=3000, S=max(S, 21), seed=S, width=96, height=72)
     h = hip_forward(hip_ext, scene, cam, S=S)
@@ -304,7 +304,7 @@ def grad_check(tag, gh, go, keys=None):
             check_grad(tag, k, gh[k], go[k], *GRAD_BARS[k])
 
 
-@pytest.mark.parametrize("S", [0, 11, 21, 24, 32])
+@pytest.mark.parametrize("S", [0, 3, 6, 11, 12, 16, 21, 24, 32])  # every SMAX instantiation
 def test_backward_matches_oracle(hip_ext, S):
     scene, cam = synthetic.small_scene(P=2500, S=max(S, 21), seed=10 + S, width=96, height=64)
     h = hip_forward(hip_ext, scene, cam, S=S)
