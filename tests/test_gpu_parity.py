@@ -427,6 +427,22 @@ def test_empty_and_culled(hip_ext):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("size", [(1, 1), (1, 40), (40, 1), (17, 5), (300, 3)])
+def test_thin_frames(hip_ext, size):
+    """Frames narrower / shorter than a tile (one partial tile row or column: the blends' inside
+    tests, the 4-tile-row xyz / normal workgroup and its edge-clamped halo, the padded launch grid):
+    forward bit-exact where the default frame is, gradients at the usual bar."""
+    W, H = size
+    scene, cam = synthetic.small_scene(P=400, S=11, seed=3, width=W, height=H)
+    h = hip_forward(hip_ext, scene, cam, S=11)
+    o = _oracle_fwd(scene, cam, 11)
+    _check_forward(h, o, 11)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=W + H)
+    gh = hip_backward(hip_ext, h, dc, do, dd, df)
+    go = oracle.rasterize_backward(o, dc, do, dd, df)
+    grad_check(f"thin {W}x{H}", gh, go)
+
+
 def test_sh_degrees(hip_ext):
     scene, cam = synthetic.small_scene(P=1500, S=3, seed=30, width=64, height=48)
     for deg in range(4):
