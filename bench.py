@@ -14,7 +14,7 @@ renders its own camera of the same scene (weak scaling).
 
 Rank 0 prints one JSON line. `roofline` prices renderCUDA fwd + bwd -- render_fwd_glds_kernel and
 render_bwd_glds_kernel with its atomic second stage (plus the sums' memset; row_sum_kernel instead
-under R3DG_BWD_REDUCE=rows) -- with SURVEY.md
+with the rows reduction, R3DG_BWD_REDUCE=rows) -- with SURVEY.md
 §8d's algorithmic bytes exactly (272*L + 156*H*W + 16*tiles at S=11; the 12*L the forward also moves
 for its fused per-tile depth sort is reported apart, as `extra_bytes`) over their device time, from HIP
 events recorded inside each launch's dispatch on the launch stream during K further steps (the
@@ -315,6 +315,8 @@ def main() -> None:
     ap.add_argument("--P", type=int, default=P_M1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=4, help="gradient exchange chunks (N > 1)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="library option (r3dg_set_options, include/r3dg_hip.h) for A/B runs, e.g. test_no_cull=1")
     args = ap.parse_args()
 
     import torch
@@ -337,6 +339,8 @@ def main() -> None:
     from relightable3dgaussian_amd import synthetic
 
     _C = r3._C
+    if args.opt:
+        _C.set_options({k: int(v) for k, v in (o.split("=", 1) for o in args.opt)})
     from relightable3dgaussian_amd import view_parallel
 
     cam = view_parallel.rank_camera(synthetic.m1_camera(W_M1, H_M1), rank, world)
@@ -425,7 +429,7 @@ def main() -> None:
     # default atomic flush: the slot times the zeroing of the per-Gaussian sums; R3DG_BWD_REDUCE=rows:
     # row_sum_kernel, which sums the partial rows the reference accumulates with atomics,
     # backward.cu:552-611)
-    reduce_mode = "rows" if os.environ.get("R3DG_BWD_REDUCE", "").startswith("r") else "atomic"
+    reduce_mode = "rows" if _C.get_options()["bwd_reduce"] == 1 else "atomic"
     t_kern = (launch["render_fwd"] + launch["render_bwd"] + launch["row_sum"]) / 1e3
     achieved = (bf + bb) / t_kern / 1e9
     traffic = None
@@ -456,7 +460,11 @@ def main() -> None:
         "views_per_s": round(world * args.steps / elapsed, 3),
         # priced against HBM (north_star: no dense contraction, the blend's bytes over 8 TB/s); which
         # resource binds is derived from the measured fractions (DESIGN.md §4 "Can 0.40 be reached")
-        "roofline": {"bound": "hbm", "binding": binding(achieved / HBM_PEAK_GBS, valu), "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "priced_against": "hbm",
+                     "bound_note": "`bound` names the peak the kernel is priced against (the contract's hbm|mfma); "
+                                   "the limiter measured from the hbm and valu fractions is `binding`",
+                     "binding": binding(achieved / HBM_PEAK_GBS, valu), "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "renderCUDA fwd + bwd: render_fwd_glds_kernel + render_bwd_glds_kernel + the reduction's "
                                "second stage (the sums memset with the default atomic flush; row_sum_kernel with "

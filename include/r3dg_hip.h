@@ -31,7 +31,8 @@
 extern "C" {
 #endif
 
-#define R3DG_ABI_VERSION 1
+/* 2: r3dg_raster_settings and r3dg_backward_outputs start with struct_size; r3dg_options */
+#define R3DG_ABI_VERSION 2
 
 enum {
     R3DG_OK = 0,
@@ -47,6 +48,41 @@ typedef void* (*r3dg_alloc_fn)(void* ctx, size_t nbytes);    /* returns device m
 int r3dg_abi_version(void);
 const char* r3dg_last_error(void);
 
+/* ---- library options (process-wide) ----------------------------------------------------------
+ * Extensible structs carry their own size as the first field: a caller sets
+ * struct_size = sizeof(the struct) as its header declares it, and the library rejects (R3DG_ERR_ARG)
+ * a struct_size it does not know, so a binding built against another version of this header, or one
+ * that forgot to zero-initialise the struct, fails loudly instead of reading garbage.
+ *
+ * No option is read from the environment on a launch. The one supported runtime option, the
+ * backward's second reduction stage, starts from R3DG_BWD_REDUCE=rows|atomic, read once when the
+ * library is loaded (default atomic); every field can be changed with r3dg_set_options. The test_*
+ * fields select cross-check, negative-test and experiment variants for the test suite and the
+ * measurement tools; production callers leave them 0. */
+enum { R3DG_REDUCE_ATOMIC = 0, R3DG_REDUCE_ROWS = 1 };
+typedef struct r3dg_options {
+    size_t struct_size;       /* sizeof(r3dg_options) */
+    int bwd_reduce;           /* R3DG_REDUCE_ATOMIC: (instance, wave) rows added into per-Gaussian sums with
+                                 atomics (default, fastest; last bits depend on arrival order, as the
+                                 reference's per-pixel atomicAdd); R3DG_REDUCE_ROWS: partial rows summed in a
+                                 fixed order, bitwise reproducible */
+    int prof_sort_markers;    /* r3dg_profile_*: also time the binning / sort stages (marker events) */
+    int test_bwd_dpp;         /* backward blend by the DPP-reduction cross-check kernel (rows reduction) */
+    int test_bwd_wterms;      /* 0 default (w in two bf16 terms); 1 / 3 (S 9..11, atomic): one term, the
+                                 inexact reduction the gradient bar must reject, or three (exact) */
+    int test_no_cull;         /* blends without the exact per-quadrant cull (same results) */
+    int test_bin_atomic;      /* the global-atomic binning (the fallback above the LDS binning's tiles) */
+    int test_bin_blocks;      /* > 0: cap on the LDS binning's workgroups (experiments) */
+    int test_tile_order_spatial; /* backward tiles in the XCD-aware spatial order, not longest first */
+    int test_bwd_srs;         /* > 0: row stride (floats) of the atomic per-Gaussian sums, rounded up to a
+                                 multiple of 8 and to at least the X part + the six f64 moments */
+    int test_bvh_lanes;       /* > 0: lanes per ray of the BVH opacity tracer (1, 2, 4, .. 64) */
+    int test_bvh_sort;        /* 0 auto (Morton-sorted rays from 256k); 1 off; 2 on */
+    int test_bvh_split;       /* 1: the static subtree-split tracer instead of the shared-stack groups */
+} r3dg_options;
+int r3dg_get_options(r3dg_options* out);   /* out->struct_size must be set */
+int r3dg_set_options(const r3dg_options* in);
+
 /* Feature output layout (replaces forward.cu:537-558, DESIGN.md "Feature layout").
  * Writes the channel-group sizes for S channels into groups[] and returns their count.
  * A group of size n starting at channel c0 is stored as a [H*W, n] block at offset c0*H*W
@@ -57,6 +93,7 @@ int r3dg_feature_groups(int S, int* groups);
 /* ---- rasterizer (rasterize_points.cu:39-181, rasterizer_impl.cu:213-529) ------------------- */
 
 typedef struct r3dg_raster_settings {
+    size_t struct_size; /* sizeof(r3dg_raster_settings) (ABI 2; checked) */
     int P;  /* number of Gaussians (means3D.size(0)) */
     int S;  /* feature channels (features.size(1)) */
     int D;  /* active SH degree */
@@ -161,6 +198,7 @@ typedef struct r3dg_backward_grads {
 } r3dg_backward_grads;
 
 typedef struct r3dg_backward_outputs {
+    size_t struct_size;   /* sizeof(r3dg_backward_outputs) (ABI 2; checked) */
     float* dL_dmeans2D;   /* [P,3] (x, y, depth) */
     float* dL_dcolors;    /* [P,3] */
     float* dL_dopacity;   /* [P,1] */
@@ -180,12 +218,11 @@ typedef struct r3dg_backward_outputs {
     void (*chunk_done)(void* ctx, int chunk, int g_begin, int g_end);
     void* chunk_ctx;
     /* Optional packed layout of the dense per-Gaussian gradients (0: dL_dmeans3D [P,3],
-     * dL_dopacity [P,1], dL_dscales [P,3], dL_drotations [P,4], dL_dfeatures [P,S] as above). A
-     * value >= 11 + S is the row stride, in floats, of all five: the caller points them at the
-     * columns 0, 3, 4, 7 and 11 of one [P, dense_stride] array, so a Gaussian range of the five is
-     * one contiguous span -- one collective per chunk for the view-parallel exchange
-     * (relightable3dgaussian_amd/view_parallel.py). Appended in round 5; zero-initialised callers
-     * keep the round-4 layout. */
+     * dL_dopacity [P,1], dL_dscales [P,3], dL_drotations [P,4], dL_dfeatures [P,S] as above). The
+     * value 11 + S (the only other one accepted) is the row stride, in floats, of all five: the
+     * caller points them at the columns 0, 3, 4, 7 and 11 of one [P, 11 + S] array, so a Gaussian
+     * range of the five is one contiguous span -- one collective per chunk for the view-parallel
+     * exchange (relightable3dgaussian_amd/view_parallel.py). */
     int dense_stride;
 } r3dg_backward_outputs;
 

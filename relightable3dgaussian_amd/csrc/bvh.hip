@@ -900,22 +900,22 @@ extern "C" int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int
     // lanes per ray (one wave's group, shared LDS stack): measured on 1M-Gaussian scenes
     // (tools/gpu_bvh_lanes*.sh), 32 lanes is best or near-best from 100k to 1M rays (1M rays:
     // 24.2 / 14.2 / 13.2 / 10.5 / 9.2 / 8.8 / 10.6 ms at 1 / 2 / ... / 64 lanes, volume scene), 64
-    // below ~32k rays; never more lanes than Gaussians. R3DG_BVH_LANES overrides (1, 2, 4, ... 64)
+    // below ~32k rays; never more lanes than Gaussians. r3dg_options.test_bvh_lanes overrides (1, 2,
+    // 4, ... 64)
+    const r3dg_options opt = options();
     int g_bits = num_rays <= 32768 ? 6 : 5;
     while (g_bits > 0 && (1ll << g_bits) > P) --g_bits;
-    if (const char* e = getenv("R3DG_BVH_LANES")) {
-        const int want = atoi(e);
+    if (opt.test_bvh_lanes > 0) {
         g_bits = 0;
-        while (g_bits < 6 && (2 << g_bits) <= want) ++g_bits;
+        while (g_bits < 6 && (2 << g_bits) <= opt.test_bvh_lanes) ++g_bits;
     }
     TraceOpacityArgs a{num_rays, P == 1 ? 1 : 0, g_bits, nrec, grec, rays_o, rays_d, num_contributes,
                        rendered_opacity, 2 * (2 * P - 1), nullptr};
     // rays in Morton order of their origins, each XCD taking a contiguous range (independent rays:
     // the results do not depend on it). Measured 1-3 % at 1M rays (8.84 -> 8.73 ms volume, 30.8 ->
     // 29.9 ms surface), a loss at 10k (the sort costs more than the locality gains), so only for
-    // >= 256k rays; R3DG_BVH_SORT=0 / 1 forces it off / on
-    const char* so = getenv("R3DG_BVH_SORT");
-    const bool sort_rays = so ? atoi(so) != 0 : num_rays >= 262144;
+    // >= 256k rays; test_bvh_sort = 1 / 2 forces it off / on
+    const bool sort_rays = opt.test_bvh_sort ? opt.test_bvh_sort == 2 : num_rays >= 262144;
     if (P > 1 && sort_rays) {
         size_t sb = 0;
         R3DG_CHECK_HIP(rocprim::radix_sort_pairs(nullptr, sb, (uint32_t*)nullptr, (uint32_t*)nullptr,
@@ -932,9 +932,8 @@ extern "C" int r3dg_bvh_trace_opacity(int num_rays, int num_gaussians, const int
         R3DG_CHECK_HIP(rocprim::radix_sort_pairs(r + 4 * b4, sb, code, code_s, idx, perm, (size_t)num_rays, 0, 30, st));
         a.perm = perm;
     }
-    // G > 1: shared-stack groups (R3DG_BVH_SPLIT=1: the static subtree split, for comparison)
-    const char* split = getenv("R3DG_BVH_SPLIT");
-    if (g_bits > 0 && !(split && atoi(split) == 1))
+    // G > 1: shared-stack groups (test_bvh_split: the static subtree split, for comparison)
+    if (g_bits > 0 && !opt.test_bvh_split)
         hipLaunchKernelGGL(bvh_trace_opacity_shared_kernel, dim3(blocks((long long)num_rays << g_bits)), dim3(256), 0,
                            st, a);
     else

@@ -95,6 +95,9 @@ ImageState image_state_from(void* base, int H, int W);
 // ---- error handling --------------------------------------------------------------------------
 void set_error(const std::string& msg);
 
+// the library options (r3dg_set_options; include/r3dg_hip.h): a snapshot, never the environment
+r3dg_options options();
+
 #define R3DG_CHECK_HIP(expr)                                                                    \
     do {                                                                                        \
         hipError_t _e = (expr);                                                                 \

@@ -149,6 +149,8 @@ struct RenderBwdArgs {
     int sums_atomic;           // 1: flush straight into `sums` with f32 atomics (no rows / flags)
     float* sums;               // [P, SRS] per-Gaussian sums, zeroed before the launch (sums_atomic)
     int SRS;
+    // kernel variant (host side; r3dg_options test_bwd_dpp / test_bwd_wterms): 0 the default
+    int variant_dpp, wterms;
 };
 
 struct GatherBwdArgs {

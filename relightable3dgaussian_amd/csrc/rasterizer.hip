@@ -28,6 +28,23 @@ namespace r3dg {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
+// ---- options (r3dg_get_options / r3dg_set_options) -------------------------------------------
+// Read by the host code of each call as one snapshot. The environment is consulted once, when the
+// library is loaded, and only for the supported runtime option R3DG_BWD_REDUCE.
+static r3dg_options initial_options() {
+    r3dg_options o{};
+    o.struct_size = sizeof(r3dg_options);
+    const char* e = getenv("R3DG_BWD_REDUCE");
+    o.bwd_reduce = (e && e[0] == 'r') ? R3DG_REDUCE_ROWS : R3DG_REDUCE_ATOMIC;
+    return o;
+}
+static std::mutex g_opt_mu;
+static r3dg_options g_options = initial_options();
+r3dg_options options() {
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    return g_options;
+}
+
 static inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 FeatureLayout make_feature_layout(int S, long long HW, bool native) {
@@ -57,11 +74,10 @@ static size_t scan_temp_size(size_t P) {
     return bytes;
 }
 
-// the backward's launch order (read per call): longest tiles first; R3DG_TILE_ORDER=xcd the
-// XCD-aware spatial order (per-XCD-band orders measured and dropped)
-static const uint32_t* bwd_tile_order(const ImageState& is) {
-    const char* e = getenv("R3DG_TILE_ORDER");
-    return (e && e[0] == 'x') ? nullptr : is.tile_order;
+// the backward's launch order: longest tiles first; test_tile_order_spatial the XCD-aware spatial
+// order (per-XCD-band orders measured and dropped)
+static const uint32_t* bwd_tile_order(const ImageState& is, const r3dg_options& opt) {
+    return opt.test_tile_order_spatial ? nullptr : is.tile_order;
 }
 
 // Carving works on an integer cursor so the same code computes sizes (base 0) and pointers.
@@ -166,14 +182,15 @@ LaunchEvents take_launch_events() {
 // A profiled stage. Kernel stages (the default) pass the events to their launch (launch_kernel,
 // r3dg_kernels.h): timestamps inside the dispatch packet, no marker packets between kernels.
 // Marker stages (library calls such as the rocPRIM sorts) record the events around the calls;
-// they are recorded only when R3DG_PROF_SORT is set, since marker packets add gaps to the stream.
+// they are recorded only with the prof_sort_markers option, since marker packets add gaps to the
+// stream.
 struct ProfScope {
     int k;
     hipStream_t st;
     bool marker;
     int idx = -1;
-    ProfScope(int kind, hipStream_t s, bool markers = false) : k(kind), st(s), marker(markers) {
-        static const bool sort_markers = getenv("R3DG_PROF_SORT") != nullptr;
+    ProfScope(int kind, hipStream_t s, bool markers = false, bool sort_markers = false)
+        : k(kind), st(s), marker(markers) {
         if (marker && !sort_markers) return;
         if (g_prof.max_records > 0 && g_prof.n[k] < g_prof.max_records) {
             idx = g_prof.n[k]++;
@@ -370,6 +387,27 @@ using namespace r3dg;
 extern "C" int r3dg_abi_version(void) { return R3DG_ABI_VERSION; }
 extern "C" const char* r3dg_last_error(void) { return g_last_error.c_str(); }
 
+extern "C" int r3dg_get_options(r3dg_options* o) {
+    R3DG_REQUIRE(o && o->struct_size == sizeof(r3dg_options), "get_options: struct_size must be sizeof(r3dg_options)");
+    *o = options();
+    return R3DG_OK;
+}
+
+extern "C" int r3dg_set_options(const r3dg_options* o) {
+    R3DG_REQUIRE(o && o->struct_size == sizeof(r3dg_options), "set_options: struct_size must be sizeof(r3dg_options)");
+    R3DG_REQUIRE(o->bwd_reduce == R3DG_REDUCE_ATOMIC || o->bwd_reduce == R3DG_REDUCE_ROWS,
+                 "set_options: bwd_reduce must be R3DG_REDUCE_ATOMIC or R3DG_REDUCE_ROWS");
+    R3DG_REQUIRE(o->test_bwd_wterms == 0 || o->test_bwd_wterms == 1 || o->test_bwd_wterms == 3,
+                 "set_options: test_bwd_wterms must be 0, 1 or 3");
+    R3DG_REQUIRE(o->test_bin_blocks >= 0 && o->test_bwd_srs >= 0 && o->test_bwd_srs <= 4096 &&
+                     o->test_bvh_lanes >= 0 && o->test_bvh_lanes <= 64 && o->test_bvh_sort >= 0 &&
+                     o->test_bvh_sort <= 2,
+                 "set_options: option out of range");
+    std::lock_guard<std::mutex> lk(g_opt_mu);
+    g_options = *o;
+    return R3DG_OK;
+}
+
 extern "C" int r3dg_feature_groups(int S, int* groups) {
     int n = 0;
     if (S == 21) {
@@ -402,6 +440,9 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
                                            int* num_rendered, r3dg_stream_t stream) {
     hipStream_t st = (hipStream_t)stream;
     R3DG_REQUIRE(s && g && out && num_rendered, "rasterize_gaussians: null argument");
+    R3DG_REQUIRE(s->struct_size == sizeof(r3dg_raster_settings),
+                 "rasterize_gaussians: settings->struct_size must be sizeof(r3dg_raster_settings) (ABI 2)");
+    const r3dg_options opt = options();
     const int P = s->P, S = s->S, H = s->H, W = s->W;
     R3DG_REQUIRE(P >= 0 && H > 0 && W > 0, "rasterize_gaussians: invalid sizes");
     R3DG_REQUIRE(S >= 0 && S <= kMaxFeatures, "rasterize_gaussians: at most 32 feature channels are supported");
@@ -618,10 +659,9 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     binning.depth_keys = geom.depth_keys;
     binning.tile_work = img.tile_work; binning.records = geom.records;
     {
-        const char* e = getenv("R3DG_BIN");  // "atomic": the global-atomic binning (tests)
-        const bool lds = bin_blocks_max(T) > 0 && !(e && e[0] == 'a');
+        const bool lds = bin_blocks_max(T) > 0 && !opt.test_bin_atomic;  // test_bin_atomic: the fallback (tests)
         int nb = bin_blocks_max(T);
-        if (const char* eb = getenv("R3DG_BIN_BLOCKS")) nb = std::max(1, std::min(nb, atoi(eb)));  // experiments
+        if (opt.test_bin_blocks > 0) nb = std::min(nb, opt.test_bin_blocks);  // experiments
         binning.nblk = lds ? std::min(nb, (P + kBinSub - 1) / kBinSub) : 0;
         binning.hist = lds && P > 0 ? img.bin_hist : nullptr;
     }
@@ -670,7 +710,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         // binning passes that need only the scan: per-tile counts, ranges, the tile order and the
         // scatter positions run on the device while the host waits for num_rendered and allocates
         {
-            ProfScope ps(R3DG_PROF_SORT, st, true);
+            ProfScope ps(R3DG_PROF_SORT, st, true, opt.prof_sort_markers);
             R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, st));
             R3DG_CHECK_LAUNCH(s->debug, st);
         }
@@ -697,7 +737,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         // every instance to its tile's next position (also records each Gaussian's first slot),
         // then every tile by (depth bits, Gaussian id): the
         // reference's 45-bit stable sort of (tile << 32 | depth bits) (rasterizer_impl.cu:366-374)
-        ProfScope ps(R3DG_PROF_SORT, st, true);
+        ProfScope ps(R3DG_PROF_SORT, st, true, opt.prof_sort_markers);
         binning.pairs = bin.pairs;
         binning.flags = nullptr;  // the rows reduction zeroes its flags itself (backward)
         R3DG_CHECK_HIP(launch_bin_scatter(binning, st));
@@ -775,7 +815,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     ra.pairs = fuse_sort ? bin.pairs : nullptr;  // fused depth sort (render_fwd_glds_kernel)
     ra.point_list_out = bin.point_list;
     ra.shader_rec = shader_rec;
-    if (const char* e = getenv("R3DG_NO_CULL")) ra.cull = (e[0] == '0');
+    ra.cull = opt.test_no_cull ? 0 : 1;
     {
         ProfScope ps(R3DG_PROF_RENDER_FWD, st);
         R3DG_CHECK_HIP(launch_render_forward(ra, splat_active, st));
@@ -839,8 +879,15 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
                                                  r3dg_stream_t stream) {
     hipStream_t st = (hipStream_t)stream;
     R3DG_REQUIRE(s && g && gr && out, "rasterize_gaussians_backward: null argument");
+    R3DG_REQUIRE(s->struct_size == sizeof(r3dg_raster_settings),
+                 "rasterize_gaussians_backward: settings->struct_size must be sizeof(r3dg_raster_settings) (ABI 2)");
+    R3DG_REQUIRE(out->struct_size == sizeof(r3dg_backward_outputs),
+                 "rasterize_gaussians_backward: out->struct_size must be sizeof(r3dg_backward_outputs) (ABI 2)");
+    const r3dg_options opt = options();
     const int P = s->P, S = s->S, H = s->H, W = s->W, L = num_rendered;
     R3DG_REQUIRE(P >= 0 && L >= 0 && S >= 0 && S <= kMaxFeatures, "rasterize_gaussians_backward: invalid sizes");
+    R3DG_REQUIRE(out->dense_stride == 0 || out->dense_stride == 11 + S,
+                 "rasterize_gaussians_backward: dense_stride must be 0 or 11 + S");
     R3DG_REQUIRE(!g->sh || P == 0 || (s->D >= 0 && s->D <= 3 && (s->D + 1) * (s->D + 1) <= s->M && s->M <= 16),
                  "rasterize_gaussians_backward: SH degree must be 0..3 with (degree+1)^2 <= M <= 16 coefficients");
     if (P == 0) return R3DG_OK;
@@ -860,19 +907,19 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     // The second stage of the per-instance reduction (backward.cu:552-611 accumulates per pixel with
     // atomics). Default: the backward blend adds each (instance, wave) row into the per-Gaussian sums
     // with f32 atomics (no partial rows, flags or row_sum_kernel; last bits depend on arrival order,
-    // as the reference's do; M1: step 2.00 -> 1.94 ms). R3DG_BWD_REDUCE=rows: partial rows summed in
-    // a fixed order by row_sum_kernel, bitwise reproducible run to run.
-    const bool atomic_sums = [] {
-        const char* e = getenv("R3DG_BWD_REDUCE");  // read per call: tests switch it at run time
-        const char* v = getenv("R3DG_BWD");          // the DPP cross-check kernel writes partial rows
-        return !(e && e[0] == 'r') && !(v && v[0] == 'd');
-    }();
+    // as the reference's do; M1: step 2.00 -> 1.94 ms). bwd_reduce = R3DG_REDUCE_ROWS: partial rows
+    // summed in a fixed order by row_sum_kernel, bitwise reproducible run to run. The DPP
+    // cross-check kernel writes partial rows.
+    const bool atomic_sums = opt.bwd_reduce != R3DG_REDUCE_ROWS && !opt.test_bwd_dpp;
     // atomic sums: [X part (f32) | 6 moments (f64) | pad] per Gaussian, rows of 32 floats (128 B) so
     // each 16-float X segment is one aligned 64-B atomic request and the moments are 8-B aligned
     // (at least the X part and the 6 double moments: XW + 12 floats per row)
     const int srs_min = 16 * bwd_xblocks(S) + 12;  // X part + 6 double moment sums
     int SRS = (std::max(RS, srs_min) + 31) & ~31;
-    if (const char* e = getenv("R3DG_BWD_SRS")) SRS = std::max(srs_min, atoi(e)) & ~7;  // A/B of the sums' row stride
+    // A/B of the sums' row stride: rounded UP to 8 floats (the f64 moments stay 8-B aligned and
+    // inside the row)
+    if (opt.test_bwd_srs > 0) SRS = (std::max(srs_min, opt.test_bwd_srs) + 7) & ~7;
+    R3DG_REQUIRE(SRS >= srs_min && SRS % 8 == 0, "rasterize_gaussians_backward: sums row stride too small");
     const size_t row_bytes = atomic_sums ? 0 : sizeof(float) * (size_t)RS * 4 * L;
     const size_t sum_bytes = sizeof(float) * (size_t)(atomic_sums ? SRS : RS) * P;
     char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + sum_bytes);
@@ -914,8 +961,10 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
         ba.dL_dpix_f = gr->dL_dout_feature;
         ba.gflay = make_feature_layout(S, HW, gr->feature_native != 0);
         ba.S = S; ba.W = W; ba.H = H; ba.grid_x = gx; ba.grid_y = gy; ba.num_tiles = T; ba.cull = 1;
-        ba.tile_order = bwd_tile_order(is);
-        if (const char* e = getenv("R3DG_NO_CULL")) ba.cull = (e[0] == '0');
+        ba.tile_order = bwd_tile_order(is, opt);
+        ba.cull = opt.test_no_cull ? 0 : 1;
+        ba.variant_dpp = opt.test_bwd_dpp;
+        ba.wterms = opt.test_bwd_wterms;
         ba.backward_geometry = backward_geometry;
         ba.RS = RS;
         ba.rows = rows;
@@ -966,8 +1015,6 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     ga.dL_dsh = (s->M > 0) ? out->dL_dsh : nullptr;
     ga.dL_dscales = out->dL_dscales;
     ga.dL_drotations = out->dL_drotations;
-    R3DG_REQUIRE(out->dense_stride == 0 || out->dense_stride >= 11 + S,
-                 "rasterize_gaussians_backward: dense_stride must be 0 or >= 11 + S");
     if (out->dense_stride > 0) {
         ga.ld_m3 = ga.ld_op = ga.ld_sc = ga.ld_rot = ga.ld_f = out->dense_stride;
     } else {

@@ -836,15 +836,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
 
 template <int SMAX>
 static hipError_t launch_bwd_s(const RenderBwdArgs& a, hipStream_t stream) {
-    // R3DG_BWD=dpp: the DPP-reduction cross-check (tests/test_gpu_parity.py); default: the
-    // DMA-staged MFMA kernel. Both write the same partial rows (the forward's contribution set).
-    const char* e = getenv("R3DG_BWD");  // read per launch: tests switch it at run time
-    const bool dpp = e && e[0] == 'd';
-    // R3DG_BWD_WTERMS=1 / 3 (S in 9..11, atomic sums only; refused otherwise): w in one bf16 term,
-    // the inexact reduction the gradient parity bar must reject, or in three (exact products), the
-    // reference point of the default two-term split's error (tests/test_gpu_parity.py)
-    const char* wt = getenv("R3DG_BWD_WTERMS");
-    const int wterms = wt && wt[0] ? wt[0] - '0' : 0;
+    // variant_dpp (r3dg_options.test_bwd_dpp): the DPP-reduction cross-check (tests/test_gpu_parity.py);
+    // default: the DMA-staged MFMA kernel. Both write the same partial rows (the forward's contribution set).
+    const bool dpp = a.variant_dpp != 0;
+    // wterms 1 / 3 (test_bwd_wterms; S in 9..11, atomic sums only; refused otherwise): w in one bf16
+    // term, the inexact reduction the gradient parity bar must reject, or in three (exact products),
+    // the reference point of the default two-term split's error (tests/test_gpu_parity.py)
+    const int wterms = a.wterms;
     const int grid = padded_tile_grid(a.num_tiles);
     if (wterms) {
         if constexpr (SMAX == 11) {

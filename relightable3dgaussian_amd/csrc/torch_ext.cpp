@@ -100,6 +100,7 @@ FwdResult rasterize_gaussians(const torch::Tensor& background, double time, doub
 
     std::vector<int64_t> passes = postProcessingPasses.value_or(std::vector<int64_t>{});
     r3dg_raster_settings s{};
+    s.struct_size = sizeof(s);
     s.P = P; s.S = S; s.D = (int)degree; s.M = shc.numel() == 0 ? 0 : (int)shc.size(1);
     s.W = W; s.H = H;
     s.tan_fovx = (float)tan_fovx; s.tan_fovy = (float)tan_fovy; s.cx = (float)cx; s.cy = (float)cy;
@@ -183,6 +184,7 @@ BwdResult backward_impl(const torch::Tensor& background, const torch::Tensor& me
     torch::Tensor rad = radii.to(dev).to(torch::kInt32).contiguous();
 
     r3dg_raster_settings s{};
+    s.struct_size = sizeof(s);
     s.P = P; s.S = S; s.D = (int)degree; s.M = M; s.W = W; s.H = H;
     s.tan_fovx = (float)tan_fovx; s.tan_fovy = (float)tan_fovy; s.scale_modifier = (float)scale_modifier;
     s.debug = debug;
@@ -196,6 +198,7 @@ BwdResult backward_impl(const torch::Tensor& background, const torch::Tensor& me
     gr.dL_dout_opacity = go.data_ptr<float>(); gr.dL_dout_depth = gd.data_ptr<float>();
     gr.dL_dout_feature = S > 0 ? gf.data_ptr<float>() : nullptr; gr.feature_native = feature_native;
     r3dg_backward_outputs o{};
+    o.struct_size = sizeof(o);
     o.dL_dmeans2D = dL_dmeans2D.data_ptr<float>(); o.dL_dcolors = dL_dcolors.data_ptr<float>();
     o.dL_dopacity = dL_dopacity.data_ptr<float>(); o.dL_dmeans3D = dL_dmeans3D.data_ptr<float>();
     o.dL_dfeatures = S > 0 ? dL_dfeatures.data_ptr<float>() : nullptr; o.dL_dcov3D = dL_dcov3D.data_ptr<float>();
@@ -878,6 +881,39 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor> trace_bvh
 
 }  // namespace
 
+
+// r3dg_get_options / r3dg_set_options (include/r3dg_hip.h) as a dict of the option fields
+#define R3DG_OPTION_FIELDS(X)                                                                         \
+    X(bwd_reduce) X(prof_sort_markers) X(test_bwd_dpp) X(test_bwd_wterms) X(test_no_cull)              \
+    X(test_bin_atomic) X(test_bin_blocks) X(test_tile_order_spatial) X(test_bwd_srs) X(test_bvh_lanes) \
+    X(test_bvh_sort) X(test_bvh_split)
+std::map<std::string, int64_t> get_options() {
+    r3dg_options o{};
+    o.struct_size = sizeof(o);
+    check(r3dg_get_options(&o), "get_options");
+    std::map<std::string, int64_t> d;
+#define X(f) d[#f] = o.f;
+    R3DG_OPTION_FIELDS(X)
+#undef X
+    return d;
+}
+// sets the given fields (the others keep their values); returns the previous options
+std::map<std::string, int64_t> set_options(const std::map<std::string, int64_t>& kv) {
+    r3dg_options o{};
+    o.struct_size = sizeof(o);
+    check(r3dg_get_options(&o), "set_options");
+    const std::map<std::string, int64_t> prev = get_options();
+    for (const auto& it : kv) {
+        bool known = false;
+#define X(f) if (it.first == #f) { o.f = (int)it.second; known = true; }
+        R3DG_OPTION_FIELDS(X)
+#undef X
+        TORCH_CHECK(known, "set_options: unknown option ", it.first);
+    }
+    check(r3dg_set_options(&o), "set_options");
+    return prev;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "MI355X-native relightable Gaussian-splat rasterizer (drop-in for r3dg_rasterization._C)";
     // the reference surface (ext.cu:21-35)
@@ -907,6 +943,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("create_shader_manager", &create_shader_manager);
     m.def("shader_manager_info", &shader_manager_info);
     m.def("abi_version", []() { return r3dg_abi_version(); });
+    m.def("get_options", &get_options);
+    m.def("set_options", &set_options);
     // training step on the device (§8f rank 3)
     m.def("adam_step", &adam_step);
     m.def("adam_step_groups", &adam_step_groups);

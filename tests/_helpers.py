@@ -143,8 +143,9 @@ def check_grad(tag, name, got, ref, rel, frac):
                 need[str(rr)] = float(max((d64 - rr * np.abs(r64)).max(), 0.0)) / m64
         with open(path, "a") as fh:
             fh.write(json.dumps({"test": tag, "grad": name, "frac": f, "rel": r, "bar_rel": rel, "bar_frac": frac,
-                                 "need_frac": need, "reduce": os.environ.get("R3DG_BWD_REDUCE", "atomic"),
-                                 "wterms": os.environ.get("R3DG_BWD_WTERMS", "2")}) + "\n")
+                                 "need_frac": need,
+                                 "reduce": "rows" if current_option("bwd_reduce") == 1 else "atomic",
+                                 "wterms": current_option("test_bwd_wterms") or 2}) + "\n")
     m = float(np.abs(np.asarray(ref)).max()) if np.asarray(ref).size else 0.0
     assert_close(f"{tag} {name}", got, ref, frac * max(m, 1e-12), rel)
 
@@ -183,23 +184,37 @@ def assert_brdf_refops(name, got, ref, grad=False, summed=False, sensitivity=Non
 import contextlib  # noqa: E402
 
 
-class rows_reduction(contextlib.ContextDecorator):
-    """Context manager / decorator: the backward's deterministic reduction (R3DG_BWD_REDUCE=rows: partial rows
-    summed in a fixed order) for tests that compare two HIP backward runs bit for bit; the default
-    atomic flush is order-dependent in the last bits, as the reference's atomics are."""
+class lib_options(contextlib.ContextDecorator):
+    """Context manager / decorator: library options (r3dg_set_options, include/r3dg_hip.h) for the
+    duration, e.g. lib_options(test_no_cull=1); the previous options are restored on exit. The
+    library reads no environment variable on a launch: tests switch variants through this API."""
+
+    def __init__(self, **kw):
+        self.kw = kw
 
     def __enter__(self):
-        import os
+        import relightable3dgaussian_amd as r
 
-        self.prev = os.environ.get("R3DG_BWD_REDUCE")
-        os.environ["R3DG_BWD_REDUCE"] = "rows"
+        self.prev = r._C.set_options(self.kw)
         return self
 
     def __exit__(self, *exc):
-        import os
+        import relightable3dgaussian_amd as r
 
-        if self.prev is None:
-            os.environ.pop("R3DG_BWD_REDUCE", None)
-        else:
-            os.environ["R3DG_BWD_REDUCE"] = self.prev
+        r._C.set_options(self.prev)
         return False
+
+
+def current_option(name):
+    import relightable3dgaussian_amd as r
+
+    return r._C.get_options()[name]
+
+
+class rows_reduction(lib_options):
+    """Context manager / decorator: the backward's deterministic reduction (bwd_reduce = rows: partial rows
+    summed in a fixed order) for tests that compare two HIP backward runs bit for bit; the default
+    atomic flush is order-dependent in the last bits, as the reference's atomics are."""
+
+    def __init__(self):
+        super().__init__(bwd_reduce=1)

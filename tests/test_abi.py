@@ -192,3 +192,64 @@ def test_integration_shim_bvh_packages():
             "assert all(hasattr(_C, n) for n in ('create_bvh', 'trace_bvh', 'trace_bvh_opacity')); print('ok')")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
+
+
+def test_options_roundtrip_and_validation(lib):
+    """r3dg_get_options / r3dg_set_options (include/r3dg_hip.h): the library reads no environment
+    variable on a launch; the test / experiment variants are switched through this struct, whose
+    struct_size and ranges are checked."""
+    from tests import _abi_ctypes as A
+
+    A.bind(lib)
+    cur = A.new(A.Options)
+    assert lib.r3dg_get_options(ctypes.byref(cur)) == 0, lib.r3dg_last_error()
+    want = "rows" if os.environ.get("R3DG_BWD_REDUCE", "").startswith("r") else "atomic"
+    assert cur.bwd_reduce == (1 if want == "rows" else 0)  # the one option seeded from the environment
+    assert all(getattr(cur, f) == 0 for f in A.OPTION_FIELDS if f != "bwd_reduce")
+    try:
+        new = A.new(A.Options, bwd_reduce=1, test_no_cull=1, test_bwd_wterms=3, test_bvh_lanes=8)
+        assert lib.r3dg_set_options(ctypes.byref(new)) == 0, lib.r3dg_last_error()
+        got = A.new(A.Options)
+        assert lib.r3dg_get_options(ctypes.byref(got)) == 0
+        assert [getattr(got, f) for f in A.OPTION_FIELDS] == [getattr(new, f) for f in A.OPTION_FIELDS]
+        for bad in (dict(struct_size=0), dict(struct_size=ctypes.sizeof(A.Options) + 8), dict(bwd_reduce=2),
+                    dict(test_bwd_wterms=2), dict(test_bvh_lanes=65), dict(test_bwd_srs=-1), dict(test_bvh_sort=3)):
+            o = A.new(A.Options, **bad)
+            assert lib.r3dg_set_options(ctypes.byref(o)) == -1, bad
+            assert lib.r3dg_last_error()
+        assert lib.r3dg_get_options(ctypes.byref(got)) == 0  # refused sets change nothing
+        assert [getattr(got, f) for f in A.OPTION_FIELDS] == [getattr(new, f) for f in A.OPTION_FIELDS]
+        stale = A.new(A.Options, struct_size=8)
+        assert lib.r3dg_get_options(ctypes.byref(stale)) == -1
+    finally:
+        assert lib.r3dg_set_options(ctypes.byref(cur)) == 0
+
+
+def test_raster_structs_checked_before_any_launch(lib):
+    """ABI 2: r3dg_raster_settings and r3dg_backward_outputs start with struct_size, and a struct
+    that is not this header's (struct_size 0 from a caller that zero-initialises an older layout, or
+    garbage) is refused with R3DG_ERR_ARG before any device work -- which is why this runs on the
+    CPU. dense_stride must be 0 or exactly 11 + S (round 5's appended field)."""
+    from tests import _abi_ctypes as A
+
+    A.bind(lib)
+    nr = ctypes.c_int(-1)
+    alloc = A.ALLOC(lambda ctx, n: None)
+    for size in (0, ctypes.sizeof(A.RasterSettings) - 8, 12345):
+        s = A.new(A.RasterSettings, P=10, S=3, W=16, H=16)
+        s.struct_size = size
+        rc = lib.r3dg_rasterize_gaussians_ex(ctypes.byref(s), ctypes.byref(A.Gaussians()),
+                                             ctypes.byref(A.ForwardOutputs()), alloc, None, alloc, None, alloc, None,
+                                             alloc, None, ctypes.byref(nr), None)
+        assert rc == -1 and b"struct_size" in lib.r3dg_last_error(), size
+    s = A.new(A.RasterSettings, P=10, S=3, W=16, H=16)
+    gr = A.BackwardGrads()
+    for kw in (dict(struct_size=0), dict(struct_size=ctypes.sizeof(A.BackwardOutputs) - 8), dict(dense_stride=1),
+               dict(dense_stride=15), dict(dense_stride=1 << 20)):
+        out = A.new(A.BackwardOutputs, **kw)
+        rc = lib.r3dg_rasterize_gaussians_backward(ctypes.byref(s), ctypes.byref(A.Gaussians()), None,
+                                                   ctypes.byref(gr), None, None, None, 0, 1, alloc, None,
+                                                   ctypes.byref(out), None)
+        assert rc == -1, kw
+        msg = lib.r3dg_last_error()
+        assert (b"struct_size" in msg) if "struct_size" in kw else (b"dense_stride" in msg), (kw, msg)

@@ -373,12 +373,13 @@ def test_create_bvh_refuses_cpu_tensors():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("lanes,split", [(1, 0), (2, 0), (8, 0), (64, 0), (4, 1), (32, 1)])
-def test_gpu_trace_opacity_lane_variants(hip_ext, lanes, split, monkeypatch):
+def test_gpu_trace_opacity_lane_variants(hip_ext, lanes, split):
     """Every lanes-per-ray setting of both group kernels (shared stack / subtree split) and the
-    one-lane reference-order kernel agree with the oracle."""
-    monkeypatch.setenv("R3DG_BVH_LANES", str(lanes))
-    monkeypatch.setenv("R3DG_BVH_SPLIT", str(split))
+    one-lane reference-order kernel agree with the oracle (r3dg_options test_bvh_lanes / _split)."""
+    from tests._helpers import lib_options
+
     sc = scene(6000, seed=lanes + 10 * split, spread=0.5)
     _, n, b, _ = hip_build(hip_ext, sc)
     o, d = rays_from(sc, 3000, seed=lanes)
-    compare_opacity(hip_ext, sc, n, b, o, d)
+    with lib_options(test_bvh_lanes=lanes, test_bvh_split=split):
+        compare_opacity(hip_ext, sc, n, b, o, d)

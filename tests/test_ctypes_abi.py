@@ -92,3 +92,133 @@ def test_trace_bvh_opacity_raw_ctypes(abi):
     assert torch.equal(contrib.reshape(-1), c_ref.reshape(-1))
     assert torch.equal(vis.reshape(-1), v_ref.reshape(-1))
     assert int(contrib.sum()) > 0
+
+
+def _raw_forward(lib, A, scene, cam, S, keep):
+    """r3dg_rasterize_gaussians_ex through ctypes (rasterize_points.cu:39-181's contract): inputs and
+    outputs as torch tensors, the three state buffers and the scratch from a torch-backed r3dg_alloc_fn
+    whose ctx names the buffer."""
+    import torch
+
+    from tests._helpers import tt
+
+    H, W = cam.height, cam.width
+    P = scene.P
+    ins = {k: tt(v) for k, v in dict(means3D=scene.means3D, features=np.ascontiguousarray(scene.features[:, :S]),
+                                     opacity=scene.opacity, scales=scene.scales, rotations=scene.rotations,
+                                     sh=scene.sh, bg=np.ones(3, np.float32), view=cam.view, view_inv=cam.view_inv,
+                                     proj=cam.proj, proj_inv=cam.proj_inv, campos=cam.campos).items()}
+    keep.append(ins)
+    f = lambda *s: torch.empty(*s, device="cuda")  # noqa: E731
+    outs = dict(color=f(H, W, 3), opacity=f(H, W, 1), depth=f(H, W, 1), stencil=f(H, W, 1), feature=f(H, W, S),
+                shader_color=f(H, W, 3), normal=f(H, W, 3), surface_xyz=f(H, W, 3),
+                radii=torch.empty(P, dtype=torch.int32, device="cuda"))
+    bufs = {}
+
+    @A.ALLOC
+    def alloc(ctx, n):
+        t = torch.empty(max(int(n), 256), dtype=torch.uint8, device="cuda")
+        bufs[ctx] = t
+        return t.data_ptr()
+
+    keep.append(alloc)
+    p = lambda t: t.data_ptr()  # noqa: E731
+    s = A.new(A.RasterSettings, P=P, S=S, D=3, M=scene.sh.shape[1], W=W, H=H, tan_fovx=cam.tanfovx,
+              tan_fovy=cam.tanfovy, cx=cam.cx, cy=cam.cy, scale_modifier=1.0, compute_pseudo_normal=1,
+              bg=p(ins["bg"]), viewmatrix=p(ins["view"]), viewmatrix_inv=p(ins["view_inv"]),
+              projmatrix=p(ins["proj"]), projmatrix_inv=p(ins["proj_inv"]), campos=p(ins["campos"]))
+    g = A.Gaussians(means3D=p(ins["means3D"]), features=p(ins["features"]), opacity=p(ins["opacity"]),
+                    scales=p(ins["scales"]), rotations=p(ins["rotations"]), sh=p(ins["sh"]))
+    o = A.ForwardOutputs(**{k: p(v) for k, v in outs.items()})
+    nr = ctypes.c_int(-1)
+    rc = lib.r3dg_rasterize_gaussians_ex(ctypes.byref(s), ctypes.byref(g), ctypes.byref(o), alloc, 1, alloc, 2, alloc,
+                                         3, alloc, 4, ctypes.byref(nr), _stream())
+    assert rc == 0, lib.r3dg_last_error()
+    torch.cuda.synchronize()
+    off = lib.r3dg_image_state_n_contrib_offset(H, W)
+    outs["n_contrib"] = bufs[3][off:off + 4 * H * W].view(torch.int32).view(H, W, 1)
+    return dict(outs=outs, ins=ins, s=s, g=g, geom=bufs[1], binning=bufs[2], image=bufs[3], L=nr.value)
+
+
+def _raw_backward(lib, A, fwd, dc, do, dd, df, keep):
+    """r3dg_rasterize_gaussians_backward through ctypes, the reference's CHW / planar gradients
+    (rasterize_points.cu:183-275)."""
+    import torch
+
+    from tests._helpers import tt
+
+    P, S, M = fwd["s"].P, fwd["s"].S, fwd["s"].M
+    grads = dict(dc=tt(dc), do=tt(do), dd=tt(dd), df=tt(df))
+    keep.append(grads)
+    f = lambda *s: torch.empty(*s, device="cuda")  # noqa: E731
+    res = dict(dL_dmeans2D=f(P, 3), dL_dcolors=f(P, 3), dL_dopacity=f(P, 1), dL_dmeans3D=f(P, 3),
+               dL_dfeatures=f(P, S), dL_dcov3D=f(P, 6), dL_dsh=f(P, M, 3), dL_dscales=f(P, 3), dL_drotations=f(P, 4))
+    scratch = []
+
+    @A.ALLOC
+    def alloc(ctx, n):
+        t = torch.empty(max(int(n), 256), dtype=torch.uint8, device="cuda")
+        scratch.append(t)
+        return t.data_ptr()
+
+    keep.append(alloc)
+    p = lambda t: t.data_ptr()  # noqa: E731
+    gr = A.BackwardGrads(dL_dout_color=p(grads["dc"]), color_hwc=0, dL_dout_opacity=p(grads["do"]),
+                         dL_dout_depth=p(grads["dd"]), dL_dout_feature=p(grads["df"]), feature_native=0)
+    out = A.new(A.BackwardOutputs, **{k: p(v) for k, v in res.items()})
+    rc = lib.r3dg_rasterize_gaussians_backward(ctypes.byref(fwd["s"]), ctypes.byref(fwd["g"]),
+                                               p(fwd["outs"]["radii"]), ctypes.byref(gr), p(fwd["geom"]),
+                                               p(fwd["binning"]), p(fwd["image"]), fwd["L"], 1, alloc, None,
+                                               ctypes.byref(out), _stream())
+    assert rc == 0, lib.r3dg_last_error()
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in res.items()}
+
+
+def test_hot_path_raw_ctypes(abi):
+    """The hot path's C ABI as a non-torch host binds it: r3dg_rasterize_gaussians_ex
+    and r3dg_rasterize_gaussians_backward through ctypes with torch-backed allocation callbacks and the
+    options switched through r3dg_set_options. Forward bit-identical to the `_C` binding; backward
+    bit-identical to `_C` on the deterministic rows reduction and within the oracle's GRAD_BARS on the
+    default atomic flush."""
+    from tests import _abi_ctypes as A
+    from tests._helpers import hip_backward, hip_forward, upstream_grads
+    from tests.test_gpu_parity import _check_forward, _oracle_fwd, grad_check
+
+    import relightable3dgaussian_amd as r3
+
+    lib = A.bind(abi)
+    S = 11
+    scene, cam = synthetic.small_scene(P=3000, S=21, seed=23, width=112, height=80)
+    keep = []
+    raw = _raw_forward(lib, A, scene, cam, S, keep)
+    ref = hip_forward(r3._C, scene, cam, S=S)
+    assert raw["L"] == ref["num_rendered"] > 0
+    for k in ("color", "opacity", "depth", "stencil", "feature", "shader_color", "normal", "surface_xyz", "radii",
+              "n_contrib"):
+        np.testing.assert_array_equal(raw["outs"][k].cpu().numpy(), ref[k].cpu().numpy(), err_msg=k)
+    o = _oracle_fwd(scene, cam, S)
+    _check_forward(dict(raw["outs"], num_rendered=raw["L"], _cam=cam, geom=raw["geom"], binning=raw["binning"],
+                        image=raw["image"]), o, S)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, S, seed=6)
+
+    saved = A.new(A.Options)
+    assert lib.r3dg_get_options(ctypes.byref(saved)) == 0
+    try:
+        rows = A.new(A.Options)
+        ctypes.memmove(ctypes.byref(rows), ctypes.byref(saved), ctypes.sizeof(A.Options))
+        rows.bwd_reduce = 1
+        assert lib.r3dg_set_options(ctypes.byref(rows)) == 0
+        assert r3._C.get_options()["bwd_reduce"] == 1  # one library instance behind ctypes and `_C`
+        g_raw = _raw_backward(lib, A, raw, dc, do, dd, df, keep)
+        g_ref = hip_backward(r3._C, ref, dc, do, dd, df)
+        for k in g_ref:
+            np.testing.assert_array_equal(g_raw[k], g_ref[k], err_msg=k)
+        rows.bwd_reduce = 0
+        assert lib.r3dg_set_options(ctypes.byref(rows)) == 0
+        g_atomic = _raw_backward(lib, A, raw, dc, do, dd, df, keep)
+    finally:
+        assert lib.r3dg_set_options(ctypes.byref(saved)) == 0
+    import oracle as orc
+
+    grad_check("raw ctypes atomic", g_atomic, orc.rasterize_backward(o, dc, do, dd, df))

@@ -14,8 +14,8 @@ import pytest
 
 import oracle
 from relightable3dgaussian_amd import synthetic
-from tests._helpers import (assert_brdf, assert_close, check_grad, hip_backward, hip_forward, rows_reduction, tt,
-                            upstream_grads)
+from tests._helpers import (assert_brdf, assert_close, check_grad, hip_backward, hip_forward, lib_options,
+                            rows_reduction, tt, upstream_grads)
 
 pytestmark = pytest.mark.gpu
 
@@ -144,14 +144,11 @@ def _cull_on_off(hip_ext, scene, cam, S=11, seed=1, atomic_keys=None):
     with rows_reduction():  # the two backward runs are compared bit for bit
         ga = hip_backward(hip_ext, a, dc, do, dd, df)
     ga_atomic = hip_backward(hip_ext, a, dc, do, dd, df)
-    os.environ["R3DG_NO_CULL"] = "1"
-    try:
+    with lib_options(test_no_cull=1):
         b = hip_forward(hip_ext, scene, cam, S=S)
         with rows_reduction():
             gb = hip_backward(hip_ext, b, dc, do, dd, df)
         gb_atomic = hip_backward(hip_ext, b, dc, do, dd, df)
-    finally:
-        del os.environ["R3DG_NO_CULL"]
     for k in ["color", "opacity", "depth", "feature", "n_contrib", "normal", "surface_xyz"]:
         np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
     for k in ga:
@@ -329,7 +326,7 @@ def test_backward_precomputed_colors_and_cov(hip_ext):
 
 
 def test_backward_deterministic(hip_ext):
-    """The deterministic reduction (R3DG_BWD_REDUCE=rows: partial rows summed in a fixed order) gives
+    """The deterministic reduction (bwd_reduce = rows: partial rows summed in a fixed order) gives
     bitwise the same gradients run to run."""
     scene, cam = synthetic.small_scene(P=3000, S=11, seed=2, width=96, height=96)
     with rows_reduction():
@@ -342,10 +339,10 @@ def test_backward_deterministic(hip_ext):
 
 
 @pytest.mark.parametrize("size", [(100, 90), (208, 160)])
-def test_backward_launch_orders(hip_ext, size, monkeypatch):
+def test_backward_launch_orders(hip_ext, size):
     """The backward's tile launch order only schedules: longest tiles first (default,
     tile_ranges_kernel; padded-grid slots past the last tile are empty) and the XCD-aware spatial
-    order (R3DG_TILE_ORDER=xcd) give bitwise the same gradients on the rows reduction. 100 x 90: 42
+    order (test_tile_order_spatial) give bitwise the same gradients on the rows reduction. 100 x 90: 42
     tiles on a 48-workgroup grid; 208 x 160: 130 tiles on 136."""
     W, H = size
     scene, cam = synthetic.small_scene(P=3000, S=11, seed=4, width=W, height=H)
@@ -354,8 +351,8 @@ def test_backward_launch_orders(hip_ext, size, monkeypatch):
     with rows_reduction():
         h = hip_forward(hip_ext, scene, cam, S=11)
         for order in ("longest", "xcd"):
-            monkeypatch.setenv("R3DG_TILE_ORDER", order)
-            g[order] = hip_backward(hip_ext, h, dc, do, dd, df)
+            with lib_options(test_tile_order_spatial=int(order == "xcd")):
+                g[order] = hip_backward(hip_ext, h, dc, do, dd, df)
     for k in g["longest"]:
         np.testing.assert_array_equal(g["xcd"][k], g["longest"][k], err_msg=k)
 
@@ -539,7 +536,7 @@ def test_binning_large_frames(hip_ext, size):
 
 @rows_reduction()
 def test_binning_atomic_path_matches(hip_ext):
-    """The global-atomic binning (R3DG_BIN=atomic, the fallback above kBinMaxTiles) and the LDS
+    """The global-atomic binning (test_bin_atomic, the fallback above kBinMaxTiles) and the LDS
     binning give bit-identical sorted lists, images and gradients; both match the oracle's keys."""
     cam = synthetic.m1_camera(480, 272)
     scene = synthetic.m1_scene(P=60_000, S=11, seed=9, cam=cam)
@@ -547,12 +544,9 @@ def test_binning_atomic_path_matches(hip_ext):
     _keys_vs_oracle(hip_ext, scene, cam, a)
     dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=2)
     ga = hip_backward(hip_ext, a, dc, do, dd, df)
-    os.environ["R3DG_BIN"] = "atomic"
-    try:
+    with lib_options(test_bin_atomic=1):
         b = hip_forward(hip_ext, scene, cam, S=11)
         gb = hip_backward(hip_ext, b, dc, do, dd, df)
-    finally:
-        del os.environ["R3DG_BIN"]
     _keys_vs_oracle(hip_ext, scene, cam, b)
     for k in ["color", "opacity", "depth", "feature", "n_contrib"]:
         np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
@@ -711,24 +705,17 @@ def test_autograd_wrapper(hip_ext):
 @pytest.mark.parametrize("reduce", ["atomic", "rows"])
 @pytest.mark.parametrize("S", [0, 11, 21, 32])
 def test_backward_reductions_match_oracle(hip_ext, S, reduce):
-    """Both second stages of the backward's reduction (R3DG_BWD_REDUCE): the per-(instance, wave)
+    """Both second stages of the backward's reduction (the bwd_reduce option): the per-(instance, wave)
     rows added straight into the per-Gaussian sums with f32 atomics, and the deterministic partial
     rows + row_sum_kernel, against the oracle; and against each other."""
     scene, cam = synthetic.small_scene(P=3000, S=max(S, 21), seed=60 + S, width=112, height=80)
     o = _oracle_fwd(scene, cam, S)
     dc, do, dd, df = upstream_grads(cam.height, cam.width, S, seed=3)
     go = oracle.rasterize_backward(o, dc, do, dd, df)
-    prev = os.environ.get("R3DG_BWD_REDUCE")
-    os.environ["R3DG_BWD_REDUCE"] = reduce
-    try:
+    with lib_options(bwd_reduce=int(reduce == "rows")):
         gh = hip_backward(hip_ext, hip_forward(hip_ext, scene, cam, S=S), dc, do, dd, df)
-        os.environ["R3DG_BWD_REDUCE"] = "rows" if reduce == "atomic" else "atomic"
+    with lib_options(bwd_reduce=int(reduce != "rows")):
         gx = hip_backward(hip_ext, hip_forward(hip_ext, scene, cam, S=S), dc, do, dd, df)
-    finally:
-        if prev is None:
-            del os.environ["R3DG_BWD_REDUCE"]
-        else:
-            os.environ["R3DG_BWD_REDUCE"] = prev
     grad_check(f"reductions {reduce} S={S}", gh, go)
     for k in go:
         if k in gh:
@@ -744,11 +731,8 @@ def test_backward_mfma_matches_dpp_variant(hip_ext, S):
     scene, cam = synthetic.small_scene(P=3000, S=21, seed=40 + S, width=96, height=80)
     dc, do, dd, df = upstream_grads(cam.height, cam.width, S)
     gm = hip_backward(hip_ext, hip_forward(hip_ext, scene, cam, S=S), dc, do, dd, df)
-    os.environ["R3DG_BWD"] = "dpp"
-    try:
+    with lib_options(test_bwd_dpp=1):
         gd = hip_backward(hip_ext, hip_forward(hip_ext, scene, cam, S=S), dc, do, dd, df)
-    finally:
-        del os.environ["R3DG_BWD"]
     for k in gm:
         assert_close(f"dpp {k}", gm[k], gd[k], 1e-5 * max(float(np.abs(gd[k]).max()) if gd[k].size else 0.0, 1e-12),
                      1e-3)
@@ -801,8 +785,9 @@ def _chunked_exchange_worker(rank, world, port, q, mode="views"):
     import torch
     import torch.distributed as dist
 
-    os.environ["R3DG_BWD_REDUCE"] = "rows"  # local and exchanged backward runs are compared bitwise
     import relightable3dgaussian_amd as r3
+
+    r3._C.set_options({"bwd_reduce": 1})  # local and exchanged backward runs are compared bitwise
     from relightable3dgaussian_amd import view_parallel
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -891,14 +876,14 @@ def test_sh_rebuild_kernels_match_oracle(hip_ext):
     np.testing.assert_allclose(got, sum(per_view_sh), rtol=1e-5, atol=1e-6 * scale)
 
 
-def test_one_term_reduction_fails_bar(hip_ext, monkeypatch):
+@lib_options(bwd_reduce=0)
+def test_one_term_reduction_fails_bar(hip_ext):
     """The gradient bar can fail: at an M1 crop (480x272 of the M1 camera, the M1 density: 63k
     Gaussians) the default backward (atomic flush, w split into two bf16 terms) meets GRAD_BARS,
-    while the one-term reduction (R3DG_BWD_WTERMS=1: w truncated to one bf16 term, ~2^-8 relative
-    per product) must violate them on the colour / feature gradients. (The WTERMS switch exists on
+    while the one-term reduction (test_bwd_wterms = 1: w truncated to one bf16 term, ~2^-8 relative
+    per product) must violate them on the colour / feature gradients. (The wterms switch exists on
     the atomic flush only: the test pins that reduction even when the suite runs under
     R3DG_BWD_REDUCE=rows.)"""
-    monkeypatch.setenv("R3DG_BWD_REDUCE", "atomic")
     cam = synthetic.m1_camera(480, 272)
     scene = synthetic.m1_scene(P=63_000, S=11, seed=4, cam=cam)
     o = _oracle_fwd(scene, cam, 11)
@@ -907,16 +892,10 @@ def test_one_term_reduction_fails_bar(hip_ext, monkeypatch):
     h = hip_forward(hip_ext, scene, cam, S=11)
     _check_forward(h, o, 11)
     grad_check("m1crop", hip_backward(hip_ext, h, dc, do, dd, df), go)
-    os.environ["R3DG_BWD_WTERMS"] = "1"
-    try:
+    with lib_options(test_bwd_wterms=1):
         g1 = hip_backward(hip_ext, h, dc, do, dd, df)
-    finally:
-        del os.environ["R3DG_BWD_WTERMS"]
-    os.environ["R3DG_BWD_WTERMS"] = "3"
-    try:  # the exact split, for the record: the default's error above this one is the split's
-        grad_check("m1crop exact-split", hip_backward(hip_ext, h, dc, do, dd, df), go)
-    finally:
-        del os.environ["R3DG_BWD_WTERMS"]
+    with lib_options(test_bwd_wterms=3):  # the exact split, for the record: the default's
+        grad_check("m1crop exact-split", hip_backward(hip_ext, h, dc, do, dd, df), go)  # error above it is the split's
     failed = []
     for k in ["dL_dcolors", "dL_dfeatures"]:
         try:
