@@ -147,7 +147,7 @@ __device__ static bool preprocess_one(const PreprocessArgs& a, int idx, const fl
     a.conic_opacity[idx] = rec0;
     a.tiles_touched[idx] = (uint32_t)((y1 - y0) * (x1 - x0));
     a.depth_keys[idx] = __float_as_uint(pv.z);
-    rec1 = make_float4(px, py, 0.0f, __int_as_float((int)my_radius));  // slot0 set by the duplicate pass
+    rec1 = make_float4(px, py, 0.0f, __int_as_float((int)my_radius));
     col = a.colors_precomp ? a.colors_precomp + 3 * idx : a.rgb + 3 * idx;
     depth = pv.z;
     return true;
@@ -233,8 +233,9 @@ __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* _
 //   4. bin_offsets_kernel: hist[b, t] = first position of workgroup b's instances of tile t;
 //   5. bin_scatter_kernel: every instance takes the next position of its (workgroup, tile) from
 //      an LDS counter and writes (depth bits, Gaussian id) there -- one 8-byte store, and the
-//      depth sort reads its keys coalesced instead of gathering them per instance (also stores
-//      each Gaussian's first slot in its render record; zeroes row flags when given them).
+//      depth sort reads its keys coalesced instead of gathering them per instance (also zeroes
+//      row flags when given them; the rows reduction reads each Gaussian's first slot from the
+//      scan, offsets[g - 1], not from a record store here: 1 M scattered 4-byte stores fewer).
 // No global atomics: they execute at the memory side (MI355X_MICROARCH.md "Global float
 // atomics"), one 64-B request per scattered lane -- a first version with one per instance took
 // 0.18 ms per pass at M1. Steps 1-4 need only the scan of tiles touched, so they run while the
@@ -248,7 +249,7 @@ __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* _
 // instance (key: the Gaussian's depth bits, scatter passes only). Every thread takes a contiguous run of the range's slots: one binary search for the
 // run's first Gaussian, then the rect walked row-major (duplicateWithKeys' order) -- the search's
 // dependent LDS reads are paid once per run, not once per instance. Scatter passes also zero the
-// backward's row flags of the range's slots (coalesced) and store each Gaussian's first slot.
+// backward's row flags of the range's slots (coalesced).
 template <class Visit>
 __device__ __forceinline__ void bin_enumerate(const BinArgs& a, int g0, int n, uint32_t* s_end, int* s_x0, int* s_y0,
                                               int* s_w, bool scatter, Visit visit) {
@@ -263,9 +264,6 @@ __device__ __forceinline__ void bin_enumerate(const BinArgs& a, int g0, int n, u
         if (r > 0) {
             const float2 m = a.means2D[g];
             get_rect(m.x, m.y, r, a.grid_x, a.grid_y, x0, y0, x1, y1);
-            if (scatter && a.records)
-                reinterpret_cast<float*>(a.records + (size_t)g * a.rec4 + 1)[2] =
-                    __uint_as_float(g == 0 ? 0u : a.offsets[g - 1]);
         }
         s_x0[i] = x0;
         s_y0[i] = y0;

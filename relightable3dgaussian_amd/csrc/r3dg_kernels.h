@@ -228,11 +228,12 @@ hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* or
                                   uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB, int min_n,
                                   hipStream_t st);
 
-// Slot of an instance from its Gaussian's render record word 1 (x, y, slot0, radius) and its tile.
-__device__ __forceinline__ uint32_t record_slot(float4 r1, int tx, int ty, int grid_x, int grid_y) {
+// Slot of an instance from its Gaussian's render record word 1 (x, y, -, radius), the Gaussian's
+// first slot slot0 = offsets[g-1] and the tile (the rows reduction's partial-row index).
+__device__ __forceinline__ uint32_t record_slot(float4 r1, uint32_t slot0, int tx, int ty, int grid_x, int grid_y) {
     int x0, y0, x1, y1;
     get_rect(r1.x, r1.y, __float_as_int(r1.w), grid_x, grid_y, x0, y0, x1, y1);
-    return __float_as_uint(r1.z) + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
+    return slot0 + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));
 }
 
 // Slot of the instance (Gaussian g, tile) in the reference's unsorted, Gaussian-contiguous order:
@@ -264,10 +265,9 @@ hipError_t launch_sh_grad_views(int g0, int n, int deg, int M, int N, const floa
 // Gaussians, so their attribute gathers hit the same L2). Grid is padded to a multiple of 8.
 // Feature-count bucket of the templated blend kernels (launch_* dispatch) and the per-Gaussian
 // render record the blend kernels stage from: float4 [conic.x, conic.y, conic.z, opacity],
-// float4 [x, y, slot0 bits, radius bits], then the attribute row [r, g, b, depth, f0 .. f_{SMAX-1}]
-// zero-padded to (4 + SMAX + 3) / 4 float4. slot0 = offsets[g-1] (the Gaussian's first unsorted
-// slot). Written by preprocess_kernel (+ slot0 by the binning scatter) for visible
-// Gaussians only; the blend kernels never stage an invisible one.
+// float4 [x, y, 0, radius bits], then the attribute row [r, g, b, depth, f0 .. f_{SMAX-1}]
+// zero-padded to (4 + SMAX + 3) / 4 float4. Written by preprocess_kernel for visible Gaussians
+// only; the blend kernels never stage an invisible one.
 __host__ __device__ inline int smax_of(int S) {
     return S == 0 ? 0 : S <= 4 ? 4 : S <= 8 ? 8 : S <= 12 ? 12 : S <= 16 ? 16 : S <= 24 ? 24 : 32;
 }

@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
             const float4 co = rec[0], r1 = rec[1];
             s_xy[t] = make_float2(r1.x, r1.y);
             s_co[t] = co;
-            s_slot[t] = record_slot(r1, tx, ty, a.grid_x, a.grid_y);
+            s_slot[t] = record_slot(r1, gid == 0 ? 0u : a.offsets[gid - 1], tx, ty, a.grid_x, a.grid_y);
             s_mask[t] = a.contrib[range.x + (uint32_t)(hi - 1 - t)];  // the forward's contribution bits
 #pragma unroll
             for (int q = 0; q < NA4; ++q) s_attr[t * NA4 + q] = rec[2 + q];
@@ -734,7 +734,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         if constexpr (ATOM) {
             row_l = gid_cur;
         } else if ((bits >> l) & 1u) {
-            const uint32_t slot = record_slot(st[NB + l], tx, ty, a.grid_x, a.grid_y);
+            const uint32_t slot =
+                record_slot(st[NB + l], gid_cur == 0 ? 0u : a.offsets[gid_cur - 1], tx, ty, a.grid_x, a.grid_y);
             row_l = 4 * slot + w;
             a.flags[row_l] = 1;
         }
