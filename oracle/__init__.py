@@ -390,6 +390,24 @@ class blend_exp_libm:
         return False
 
 
+class power_ref_ops:
+    """Context manager: the oracle's blend evaluates the Gaussian's power with the reference's
+    operation order (forward.cu:478; mode 1 as written, mode 2 with nvcc's default contractions)
+    instead of the staged FMA pattern the HIP kernels share with it (measures that choice,
+    DESIGN.md §5)."""
+
+    def __init__(self, mode=1):
+        self.mode = mode
+
+    def __enter__(self):
+        lib().oracle_set_power_ref_ops(ctypes.c_int(self.mode))
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_power_ref_ops(ctypes.c_int(0))
+        return False
+
+
 def expf_accuracy(lo=-80.0, hi=0.0, stride=1):
     """(max ulp error, n, correctly rounded count) of r3dg_expf against double exp over every
     `stride`-th float in [lo, hi]."""

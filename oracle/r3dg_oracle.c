@@ -73,8 +73,24 @@ static void get_rect(float px, float py, int max_radius, int gx, int gy, int* rm
 /* forward.cu:468 / backward.cu:526: -0.5f * (a dx^2 + c dy^2) - b dx dy as one fixed FMA pattern
  * (the HIP kernels' gauss_power, r3dg_common.h): with the staged conic (A, B, C) = (-a/2, -b, -c/2)
  * (exact scalings, preprocess_kernel's render records), dx (A dx + B dy) + C dy^2. */
+static int g_power_ref_ops = 0;
+/* Measurement switch (tests/test_oracle.py test_power_ref_ops_c2): 0 = the staged
+ * FMA pattern below (the HIP kernels'); 1 = forward.cu:478 / backward.cu:526 as written,
+ * -0.5f * (a dx dx + c dy dy) - b dx dy, every product and sum rounded (no contraction); 2 = the
+ * same expression with the two contractions nvcc's default -fmad=true may apply
+ * (fma(a dx, dx, (c dy) dy), then fma(-0.5, s, -(b dx) dy)). The reference's own bits depend on
+ * its compiler; these bracket them. */
+void oracle_set_power_ref_ops(int mode) { g_power_ref_ops = mode; }
 static float gauss_power(const float* co, float dx, float dy)
 {
+    if (g_power_ref_ops == 1) {
+        const float s = co[0] * dx * dx + co[2] * dy * dy;
+        return -0.5f * s - co[1] * dx * dy;
+    }
+    if (g_power_ref_ops == 2) {
+        const float s = fmaf(co[0] * dx, dx, (co[2] * dy) * dy);
+        return fmaf(-0.5f, s, -((co[1] * dx) * dy));
+    }
     const float A = -0.5f * co[0], B = -co[1], C = -0.5f * co[2];
     const float f = fmaf(A, dx, B * dy);
     return fmaf(dx, f, (C * dy) * dy);

@@ -253,3 +253,60 @@ def test_raster_structs_checked_before_any_launch(lib):
         assert rc == -1, kw
         msg = lib.r3dg_last_error()
         assert (b"struct_size" in msg) if "struct_size" in kw else (b"dense_stride" in msg), (kw, msg)
+
+
+def _kernel_resources():
+    """{demangled kernel name: metadata} of every gfx950 kernel in the built library (its
+    .hip_fatbin section holds one offload bundle per source file)."""
+    import subprocess
+    import tempfile
+
+    import yaml
+
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(f"{llvm}/llvm-readelf"):
+        pytest.skip("ROCm llvm tools not found")
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={d}/fb.bin", LIB], check=True)
+        data = open(f"{d}/fb.bin", "rb").read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        starts, i = [], data.find(magic)
+        while i >= 0:
+            starts.append(i)
+            i = data.find(magic, i + 1)
+        for n, s in enumerate(starts):
+            e = starts[n + 1] if n + 1 < len(starts) else len(data)
+            open(f"{d}/b{n}.bin", "wb").write(data[s:e])
+            subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={d}/b{n}.bin",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={d}/k{n}.co"], check=True)
+            notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", f"{d}/k{n}.co"], check=True,
+                                   capture_output=True, text=True).stdout
+            if "---" not in notes:
+                continue
+            meta = yaml.safe_load(notes[notes.index("---"):notes.rindex("...") + 3])
+            for k in meta.get("amdhsa.kernels", []):
+                name = subprocess.run(["c++filt", k[".name"]], capture_output=True, text=True).stdout.strip()
+                out[name] = k
+    return out
+
+
+def test_blend_kernel_occupancy_budget():
+    """The blend kernels' occupancy is set by registers and LDS together; a code or
+    compiler change that tips one over a step would silently lose a wave per SIMD. Pinned here from
+    the built code objects: render_bwd_glds_kernel<11, true, 2> (M1's backward) <= 128 VGPRs and
+    <= 40 KiB of LDS (4 workgroups = 4 waves per SIMD), render_fwd_glds_kernel<11, false> <= 64
+    VGPRs, <= 80 SGPRs (MI355X_MICROARCH.md: 82-96 SGPRs admit 7 workgroups of 256 per CU) and
+    <= 20 KiB of LDS (8 waves per SIMD); neither spills."""
+    res = _kernel_resources()
+    budgets = {"void r3dg::render_bwd_glds_kernel<11, true, 2>(r3dg::RenderBwdArgs)": (128, 102, 40960),
+               "void r3dg::render_fwd_glds_kernel<11, false>(r3dg::RenderFwdArgs)": (64, 80, 20480)}
+    for name, (vg, sg, lds) in budgets.items():
+        assert name in res, (name, sorted(k for k in res if "render_" in k))
+        k = res[name]
+        print(f"{name}: vgpr {k['.vgpr_count']} sgpr {k['.sgpr_count']} lds {k['.group_segment_fixed_size']}")
+        assert k[".vgpr_count"] + k.get(".agpr_count", 0) <= vg, name
+        assert k[".sgpr_count"] <= sg, name
+        assert k[".group_segment_fixed_size"] <= lds, name
+        assert k.get(".vgpr_spill_count", 0) == 0 and k.get(".sgpr_spill_count", 0) == 0, name
+        assert k[".private_segment_fixed_size"] == 0, name

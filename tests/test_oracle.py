@@ -192,6 +192,36 @@ def test_blend_exp_choice_c2():
     assert nc < 1e-4 and dT < 1e-4
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_power_ref_ops_c2(mode):
+    """How far the blend's outputs move when the Gaussian's power is evaluated in the reference's
+    operation order (forward.cu:478, -0.5f * (a dx dx + c dy dy) - b dx dy: mode 1 every operation
+    rounded, mode 2 with nvcc's default contractions) instead of the staged-conic FMA pattern the
+    HIP kernels and the oracle share (r3dg_common.h gauss_power). C2-sized frame, both oracle runs
+    on the same binning. The images stay within north_star's 1e-4 bar; the fractions of pixels whose
+    n_contrib / final_T bits change are reported and bounded: this is the distance
+    between the pinned restatement and the reference's own arithmetic, which no reference file pins."""
+    cam = synthetic.orbit_camera(0.0, 30.0, 4.0311, 0.6911112, 800, 800)
+    scene = synthetic.ball_scene(300_000, S=21, seed=0)
+    args = dict(sh=scene.sh, scales=scene.scales, rotations=scene.rotations)
+    a = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features, **args)
+    with oracle.power_ref_ops(mode):
+        b = oracle.rasterize_forward(cam, scene.means3D, scene.opacity, scene.features, **args)
+    np.testing.assert_array_equal(a["point_list"], b["point_list"])  # binning does not use the power
+    npix = a["final_T"].size
+    nc = float((a["n_contrib"] != b["n_contrib"]).mean())
+    ft = float((a["final_T"] != b["final_T"]).mean())
+    dT = float(np.abs(a["final_T"].astype(np.float64) - b["final_T"]).max())
+    print(f"\npower staged FMA vs reference order (mode {mode}), C2 ({npix} px): n_contrib differs on {nc:.3e} "
+          f"of pixels, final_T bits on {ft:.3e} (max |dT| {dT:.2e})")
+    for k in ["color", "opacity", "depth", "feature"]:
+        d = np.abs(a[k].astype(np.float64) - b[k])
+        print(f"  max |d {k}| = {float(d.max()):.2e}")
+        scale = np.maximum(1.0, np.abs(a[k].astype(np.float64))) if k == "depth" else 1.0
+        assert float((d / scale).max()) <= 1e-4, (k, float(d.max()))
+    assert nc < 1e-3 and dT < 1e-4
+
+
 def test_binning_invariants():
     """duplicateWithKeys / sort / identifyTileRanges (rasterizer_impl.cu:58-141)."""
     scene, cam, o = _small()
