@@ -903,3 +903,24 @@ def test_one_term_reduction_fails_bar(hip_ext):
         except AssertionError:
             failed.append(k)
     assert failed == ["dL_dcolors", "dL_dfeatures"], failed
+
+
+def test_backward_uses_sums_prepared_by_forward(hip_ext):
+    """A training forward zeroes the backward's atomic sums inside its blend (RenderFwdArgs::zero_sums,
+    no memset launch in the backward). The first backward on that forward uses them; a second one on
+    the same forward finds them used and zeroes scratch itself: both agree with each other and with
+    the oracle, also on a second forward at the same size."""
+    scene, cam = synthetic.small_scene(P=3000, S=11, seed=52, width=112, height=80)
+    o = _oracle_fwd(scene, cam, 11)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=9)
+    go = oracle.rasterize_backward(o, dc, do, dd, df)
+    with lib_options(bwd_reduce=0):
+        h = hip_forward(hip_ext, scene, cam, S=11)
+        g1 = hip_backward(hip_ext, h, dc, do, dd, df)   # the prepared sums
+        g2 = hip_backward(hip_ext, h, dc, do, dd, df)   # used: memset path
+        h2 = hip_forward(hip_ext, scene, cam, S=11)
+        g3 = hip_backward(hip_ext, h2, dc, do, dd, df)
+    for g in (g1, g2, g3):
+        grad_check("prepared sums", g, go)
+    assert_hip_runs_agree("prepared vs memset", g1, g2)
+    assert_hip_runs_agree("second forward", g1, g3)
