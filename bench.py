@@ -426,7 +426,7 @@ def main() -> None:
     avg = {k: v[1] / args.steps for k, v in prof.items()}
     launch = {k: (v[1] / v[0] if v[0] else 0.0) for k, v in prof.items()}
     # renderCUDA fwd + bwd: the backward blend AND its per-instance reduction's second stage (the
-    # default atomic flush: the slot times the zeroing of the per-Gaussian sums; R3DG_BWD_REDUCE=rows:
+    # default atomic flush: the sums are zeroed inside render_fwd, the slot is empty; rows reduction:
     # row_sum_kernel, which sums the partial rows the reference accumulates with atomics,
     # backward.cu:552-611)
     reduce_mode = "rows" if _C.get_options()["bwd_reduce"] == 1 else "atomic"
@@ -475,7 +475,10 @@ def main() -> None:
         "kernel_ms": {("bwd_reduce_" + reduce_mode if k == "row_sum" else k): round(v, 4) for k, v in avg.items()
                       if prof[k][0]},
         "bwd_reduce": {"mode": reduce_mode,
-                       "stage": "hipMemsetAsync of the per-Gaussian sums (atomic flush inside render_bwd)"
+                       "stage": ("the per-Gaussian sums are zeroed inside render_fwd (the training forward "
+                                 "prepares them) and summed by render_bwd's atomic flush: no separate launch"
+                                 if not prof["row_sum"][0] else "hipMemsetAsync of the per-Gaussian sums + the atomic "
+                                 "flush inside render_bwd")
                        if reduce_mode == "atomic" else "row_sum_kernel over the partial rows"},
     }
     if exchange is not None:

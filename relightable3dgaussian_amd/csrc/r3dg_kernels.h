@@ -92,6 +92,11 @@ struct RenderFwdArgs {
     float* out_feature;
     float* out_shader_color;
     float* zero_stencil;  // stencil output to zero (default splat shaders), or null
+    // the backward's per-Gaussian atomic sums (in the geometry state), zeroed here so the backward
+    // needs no memset: tile t's workgroup zeroes float4s [t * zero_chunk, (t + 1) * zero_chunk) of
+    // the zero_n4 after its outputs (the stores drain under the other workgroups' blends); null: none
+    float4* zero_sums;
+    uint32_t zero_n4, zero_chunk;
     uint8_t* contrib;     // [L] per sorted position: bit q set when a pixel of quadrant q blended it
     FeatureLayout flay;
     // fused depth sort (default-shader kernel): tiles of up to kFusedSortMax instances are sorted

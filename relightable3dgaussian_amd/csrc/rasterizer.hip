@@ -74,6 +74,45 @@ static size_t scan_temp_size(size_t P) {
     return bytes;
 }
 
+// ---- the backward's atomic sums, prepared by the forward (RenderFwdArgs::zero_sums) -------------
+// Row stride (floats) of the per-Gaussian sums of the atomic flush: [X part (f32) | 6 moments (f64) |
+// pad], rows of 32 floats (128 B) so each 16-float X segment is one aligned 64-B atomic request and
+// the moments are 8-B aligned (at least the X part and the 6 double moments: XW + 12 floats per row);
+// test_bwd_srs (A/B) rounds up to 8 floats.
+static int atomic_sums_min_stride(int S) { return 16 * bwd_xblocks(S) + 12; }
+static int atomic_sums_stride(int S, const r3dg_options& opt) {
+    const int srs_min = atomic_sums_min_stride(S);
+    if (opt.test_bwd_srs > 0) return (std::max(srs_min, opt.test_bwd_srs) + 7) & ~7;
+    return (std::max(part_row_stride(S), srs_min) + 31) & ~31;
+}
+// A training forward (atomic reduction, no shaders / post passes) appends the sums to its geometry
+// state and has its blend zero them (the stores drain under the blend, which waits on latency, not
+// on memory), so the backward launches no memset (M1: the 128 MB fill, 17 us per step). The host
+// records which geometry states hold such still-zero sums; the first backward on one uses them,
+// any other backward (a second one on the same state, other options) zeroes scratch as before.
+struct PreparedSums {
+    float* sums;
+    int P, S, SRS;
+    bool fresh;
+};
+static std::mutex g_sums_mu;
+static std::map<uintptr_t, PreparedSums> g_sums;  // key: geometry state base
+static void note_prepared_sums(void* geom, const PreparedSums* ps) {
+    std::lock_guard<std::mutex> lk(g_sums_mu);
+    g_sums.erase((uintptr_t)geom);  // a new forward's state at a reused address replaces the old entry
+    if (!ps) return;
+    if (g_sums.size() >= 4096) g_sums.clear();  // entries are hints: a missing one costs a memset
+    g_sums[(uintptr_t)geom] = *ps;
+}
+static float* take_prepared_sums(void* geom, int P, int S, int SRS) {
+    std::lock_guard<std::mutex> lk(g_sums_mu);
+    auto it = g_sums.find((uintptr_t)geom);
+    if (it == g_sums.end() || !it->second.fresh || it->second.P != P || it->second.S != S || it->second.SRS != SRS)
+        return nullptr;
+    it->second.fresh = false;
+    return it->second.sums;
+}
+
 // the backward's launch order: longest tiles first; test_tile_order_spatial the XCD-aware spatial
 // order (per-XCD-band orders measured and dropped)
 static const uint32_t* bwd_tile_order(const ImageState& is, const r3dg_options& opt) {
@@ -575,7 +614,13 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     // shaders' / intermediate pass's per-Gaussian records (112 MB at 1M Gaussians with S = 21).
     const bool use_scratch = scratch_alloc != nullptr && P > 0;
     const size_t rec_bytes = sizeof(float) * (shrec_floats + inter_floats);
-    void* geom_base = geom_alloc(geom_ctx, geom_bytes + sizeof(float) * shrec_off + (use_scratch ? 0 : rec_bytes));
+    // a training forward prepares the backward's zeroed atomic sums at the end of its geometry state
+    const bool prep_sums = P > 0 && opt.bwd_reduce == R3DG_REDUCE_ATOMIC && !opt.test_bwd_dpp && !work_copies &&
+                           post_ids.empty() && !splat_active;
+    const int sums_srs = atomic_sums_stride(S, opt);
+    const size_t extra_bytes = align256(sizeof(float) * shrec_off + (use_scratch ? 0 : rec_bytes));
+    const size_t sums_bytes = prep_sums ? sizeof(float) * (size_t)sums_srs * (size_t)P : 0;
+    void* geom_base = geom_alloc(geom_ctx, geom_bytes + extra_bytes + sums_bytes);
     void* img_base = image_alloc(image_ctx, image_state_bytes(H, W, !use_scratch));
     const size_t hist_bytes = (4 * bin_hist_count((size_t)T) + 255) & ~(size_t)255;
     char* scratch_base = use_scratch ? (char*)scratch_alloc(scratch_ctx, hist_bytes + rec_bytes) : nullptr;
@@ -587,6 +632,8 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     char* rec_base = use_scratch ? scratch_base + hist_bytes
                                  : static_cast<char*>(geom_base) + geom_bytes + sizeof(float) * shrec_off;
     GeomState geom = geom_state_from(geom_base, (size_t)P, S);
+    float* prepared_sums = prep_sums ? reinterpret_cast<float*>(static_cast<char*>(geom_base) + geom_bytes + extra_bytes)
+                                     : nullptr;
     float4* shader_rec = splat_active ? reinterpret_cast<float4*>(rec_base) : nullptr;
     float4* inter_rec = inter_floats ? reinterpret_cast<float4*>(rec_base + sizeof(float) * shrec_floats) : nullptr;
     const bool hist_scratch = use_scratch;
@@ -816,6 +863,11 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     ra.point_list_out = bin.point_list;
     ra.shader_rec = shader_rec;
     ra.cull = opt.test_no_cull ? 0 : 1;
+    if (prepared_sums && T > 0) {
+        ra.zero_sums = reinterpret_cast<float4*>(prepared_sums);
+        ra.zero_n4 = (uint32_t)((size_t)sums_srs * (size_t)P / 4);
+        ra.zero_chunk = (ra.zero_n4 + (uint32_t)T - 1) / (uint32_t)T;
+    }
     {
         ProfScope ps(R3DG_PROF_RENDER_FWD, st);
         R3DG_CHECK_HIP(launch_render_forward(ra, splat_active, st));
@@ -848,6 +900,12 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
                                    : nullptr;
         R3DG_CHECK_HIP(launch_post_passes(post_ids.data(), (int)post_ids.size(), pp, scratch, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
+    }
+    if (prepared_sums && T > 0) {
+        const PreparedSums ps{prepared_sums, P, S, sums_srs, true};
+        note_prepared_sums(geom_base, &ps);
+    } else {
+        note_prepared_sums(geom_base, nullptr);
     }
     *num_rendered = L;
     return R3DG_OK;
@@ -911,25 +969,22 @@ extern "C" int r3dg_rasterize_gaussians_backward(const r3dg_raster_settings* s, 
     // summed in a fixed order by row_sum_kernel, bitwise reproducible run to run. The DPP
     // cross-check kernel writes partial rows.
     const bool atomic_sums = opt.bwd_reduce != R3DG_REDUCE_ROWS && !opt.test_bwd_dpp;
-    // atomic sums: [X part (f32) | 6 moments (f64) | pad] per Gaussian, rows of 32 floats (128 B) so
-    // each 16-float X segment is one aligned 64-B atomic request and the moments are 8-B aligned
-    // (at least the X part and the 6 double moments: XW + 12 floats per row)
-    const int srs_min = 16 * bwd_xblocks(S) + 12;  // X part + 6 double moment sums
-    int SRS = (std::max(RS, srs_min) + 31) & ~31;
-    // A/B of the sums' row stride: rounded UP to 8 floats (the f64 moments stay 8-B aligned and
-    // inside the row)
-    if (opt.test_bwd_srs > 0) SRS = (std::max(srs_min, opt.test_bwd_srs) + 7) & ~7;
+    // atomic sums: [X part (f32) | 6 moments (f64) | pad] per Gaussian (atomic_sums_stride), zeroed
+    // by the forward's blend when it prepared them (take_prepared_sums), else here
+    const int srs_min = atomic_sums_min_stride(S);
+    const int SRS = atomic_sums_stride(S, opt);
     R3DG_REQUIRE(SRS >= srs_min && SRS % 8 == 0, "rasterize_gaussians_backward: sums row stride too small");
+    float* prepared = atomic_sums ? take_prepared_sums(geom, P, S, SRS) : nullptr;
     const size_t row_bytes = atomic_sums ? 0 : sizeof(float) * (size_t)RS * 4 * L;
     const size_t sum_bytes = sizeof(float) * (size_t)(atomic_sums ? SRS : RS) * P;
-    char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + sum_bytes);
+    char* scratch = (char*)scratch_alloc(scratch_ctx, row_bytes + (prepared ? 0 : sum_bytes));
     if (!scratch) {
         set_error("rasterize_gaussians_backward: scratch allocation failed");
         return R3DG_ERR_ALLOC;
     }
     float* rows = L > 0 && !atomic_sums ? reinterpret_cast<float*>(scratch) : nullptr;
-    float* sums = reinterpret_cast<float*>(scratch + row_bytes);
-    if (atomic_sums) {
+    float* sums = prepared ? prepared : reinterpret_cast<float*>(scratch + row_bytes);
+    if (atomic_sums && !prepared) {
         ProfScope ps(R3DG_PROF_ROW_SUM, st);
         R3DG_CHECK_HIP(hipMemsetAsync(sums, 0, sum_bytes, st));
     }

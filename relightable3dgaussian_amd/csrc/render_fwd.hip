@@ -279,6 +279,11 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         write_bits(b0, n - b0, buf ^ 1);
     }
 
+    // the backward's atomic sums (RenderFwdArgs::zero_sums): this tile's share, after its blend
+    if (!SHADER && a.zero_sums) {  // (training forwards only: never with splat shaders)
+        const uint32_t z0 = (uint32_t)tile * a.zero_chunk, z1 = min(z0 + a.zero_chunk, a.zero_n4);
+        for (uint32_t i = z0 + (uint32_t)t; i < z1; i += kBlock) a.zero_sums[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     if (inside) {
         const int pix = py * a.W + px;
         a.final_T[pix] = T;
