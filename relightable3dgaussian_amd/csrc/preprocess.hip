@@ -227,18 +227,19 @@ __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* _
 // tile_depth_sort_kernel then orders every tile by (depth bits, Gaussian id):
 //   1. bin_count_kernel: workgroup b (one per CU) counts the instances of its Gaussian range per
 //      tile with LDS counters and writes its row hist[b, :];
-//   2. bin_totals_kernel: per-tile totals (column sums of hist);
+//   2. bin_colscan_kernel: per-tile totals and, in place, each workgroup's offset inside its tiles
+//      (column prefix sums of hist);
 //   3. tile_ranges_kernel: exclusive scan of the totals -> ranges (the reference's (0, 0) for
-//      empty tiles), each tile's first position, and the longest-first tile order;
-//   4. bin_offsets_kernel: hist[b, t] = first position of workgroup b's instances of tile t;
-//   5. bin_scatter_kernel: every instance takes the next position of its (workgroup, tile) from
+//      empty tiles) and each tile's first position;
+//   4. bin_scatter_kernel: every instance takes the next position of its (workgroup, tile) from
 //      an LDS counter and writes (depth bits, Gaussian id) there -- one 8-byte store, and the
 //      depth sort reads its keys coalesced instead of gathering them per instance (also zeroes
 //      row flags when given them; the rows reduction reads each Gaussian's first slot from the
-//      scan, offsets[g - 1], not from a record store here: 1 M scattered 4-byte stores fewer).
+//      scan, offsets[g - 1], not from a record store here: 1 M scattered 4-byte stores fewer);
+//      one extra workgroup of its grid computes the longest-first tile order meanwhile.
 // No global atomics: they execute at the memory side (MI355X_MICROARCH.md "Global float
 // atomics"), one 64-B request per scattered lane -- a first version with one per instance took
-// 0.18 ms per pass at M1. Steps 1-4 need only the scan of tiles touched, so they run while the
+// 0.18 ms per pass at M1. Steps 1-3 need only the scan of tiles touched, so they run while the
 // host reads num_rendered back and allocates the binning state. Workgroups enumerate their
 // instances load-balanced, kBinSub Gaussians at a time: slot q finds its Gaussian by binary search
 // over the staged instance offsets, and its tile is the row-major index of q - the Gaussian's first
@@ -328,28 +329,13 @@ __global__ void __launch_bounds__(kBinThreads) bin_count_kernel(BinArgs a) {
     for (int i = threadIdx.x; i < a.T; i += kBinThreads) row[i] = s_cnt[i];
 }
 
-// tile_work[t] = sum over workgroups of hist[b, t]: 64 tiles per workgroup (one per lane), wave w
-// of 16 sums rows w, w + 16, ... (16 independent loads in flight per wave for 256 rows)
-__global__ void __launch_bounds__(1024) bin_totals_kernel(BinArgs a) {
-    __shared__ uint32_t s_part[16][64];
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int tile = blockIdx.x * 64 + l;
-    uint32_t s = 0;
-    if (tile < a.T)
-        for (int b = w; b < a.nblk; b += 16) s += a.hist[(size_t)b * a.T + tile];
-    s_part[w][l] = s;
-    __syncthreads();
-    if (w == 0 && tile < a.T) {
-        uint32_t tot = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) tot += s_part[k][l];
-        a.tile_work[tile] = tot;
-    }
-}
-
-// hist[b, t] = tile_work[t] (the tile's first position) + sum of hist[b', t] for b' < b: 64 tiles
-// per workgroup, wave w of 16 owns the contiguous rows [w nblk / 16, (w + 1) nblk / 16)
-__global__ void __launch_bounds__(1024) bin_offsets_kernel(BinArgs a) {
+// Column scan of the per-workgroup tile counts: hist[b, t] = sum of hist[b', t] over b' < b (workgroup
+// b's first position inside tile t's range) and tile_work[t] = the column total (the tile's
+// instance count, which tile_ranges_kernel turns into its first position). 64 tiles per workgroup
+// (one per lane), wave w of 16 owns the contiguous rows [w nblk / 16, (w + 1) nblk / 16). One launch
+// for what were two (the totals, then the offsets after the ranges: round 6, one kernel boundary
+// fewer on the binning's critical path); the scatter adds the tile's first position.
+__global__ void __launch_bounds__(1024) bin_colscan_kernel(BinArgs a) {
     __shared__ uint32_t s_part[16][64];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int tile = blockIdx.x * 64 + l;
@@ -360,8 +346,9 @@ __global__ void __launch_bounds__(1024) bin_offsets_kernel(BinArgs a) {
     s_part[w][l] = s;
     __syncthreads();
     if (tile >= a.T) return;
-    uint32_t run = a.tile_work[tile];
+    uint32_t run = 0;
     for (int k = 0; k < w; ++k) run += s_part[k][l];
+    if (w == 15) a.tile_work[tile] = run + s;  // the column total
     for (int b = r0; b < r1; ++b) {
         uint32_t* h = a.hist + (size_t)b * a.T + tile;
         const uint32_t c = *h;
@@ -370,7 +357,58 @@ __global__ void __launch_bounds__(1024) bin_offsets_kernel(BinArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(kBinThreads) bin_scatter_kernel(BinArgs a) {
+// Longest-first launch order of the tiles (the backward, the long-tile depth sort): a bucket sort by
+// instance count (bucket = count / 4, capped; descending). Only the schedule depends on the order,
+// so the order within a bucket, which LDS atomics leave unspecified, changes no result (measured:
+// exact-count buckets, which scatter the tiles of a bucket spatially, slowed the backward by 3 %).
+// One 1024-thread workgroup; the padded grid's last slots name no tile (T).
+__device__ __forceinline__ uint32_t block_exclusive_scan_1024(uint32_t v, uint32_t* s_wave);
+__device__ void tile_order_block(int T, const uint2* __restrict__ ranges, uint32_t* __restrict__ order) {
+    constexpr int NBK = 1024;
+    __shared__ uint32_t hist[NBK];
+    __shared__ uint32_t s_wave[16];
+    const int t = threadIdx.x;
+    const int per = (T + 1023) / 1024;
+    const int b0 = min(t * per, T), b1 = min(b0 + per, T);
+    auto bucket = [](uint32_t c) { return (int)min(c >> 2, (uint32_t)(NBK - 1)); };
+    hist[t] = 0;
+    __syncthreads();
+    for (int i = b0; i < b1; ++i) {
+        const uint2 r = ranges[i];
+        atomicAdd(&hist[bucket(r.y - r.x)], 1u);
+    }
+    __syncthreads();
+    // exclusive scan in descending bucket order (over the reversed histogram)
+    const uint32_t v = hist[NBK - 1 - t];
+    const uint32_t ex = block_exclusive_scan_1024(v, s_wave);
+    hist[NBK - 1 - t] = ex;  // now the cursor of bucket NBK-1-t
+    __syncthreads();
+    for (int i = b0; i < b1; ++i) {
+        const uint2 r = ranges[i];
+        order[atomicAdd(&hist[bucket(r.y - r.x)], 1u)] = (uint32_t)i;
+    }
+    const int TP = padded_tile_grid(T);
+    if (t < TP - T) order[T + t] = (uint32_t)T;
+}
+
+// tile_order_block on its own, when the LDS binning scattered nothing (no instances)
+__global__ void __launch_bounds__(1024) tile_order_kernel(int T, const uint2* __restrict__ ranges,
+                                                          uint32_t* __restrict__ order) {
+    tile_order_block(T, ranges, order);
+}
+
+// The scatter grid has one workgroup more than the binning's: it computes the tiles' longest-first
+// order (tile_order_block) beside the scatter, off the binning's critical path (round 6: the ranges
+// kernel 14.9 -> 11.5 us). (Every scatter workgroup scanning the tile counts itself, so that no
+// ranges kernel runs at all, measured slower: the scatter 69 -> 80 us, and the host, which must
+// allocate the binning state between the count readback and the scatter launch, then left the GPU
+// idle 6 us; profiles/r06/README.md.)
+__global__ void __launch_bounds__(kBinThreads) bin_scatter_kernel(BinArgs a, const uint2* __restrict__ ranges,
+                                                                  uint32_t* __restrict__ order) {
+    if ((int)blockIdx.x == a.nblk) {
+        tile_order_block(a.T, ranges, order);
+        return;
+    }
     extern __shared__ uint32_t s_dyn[];
     uint32_t* s_pos = s_dyn;  // [T] next position of this workgroup's instances of each tile
     uint32_t* s_end = s_dyn + a.T;
@@ -378,7 +416,8 @@ __global__ void __launch_bounds__(kBinThreads) bin_scatter_kernel(BinArgs a) {
     int* s_y0 = s_x0 + kBinSub;
     int* s_w = s_y0 + kBinSub;
     const uint32_t* row = a.hist + (size_t)blockIdx.x * a.T;
-    for (int i = threadIdx.x; i < a.T; i += kBinThreads) s_pos[i] = row[i];
+    // the workgroup's first position in each tile: the tile's first position + its column offset
+    for (int i = threadIdx.x; i < a.T; i += kBinThreads) s_pos[i] = a.tile_work[i] + row[i];
     int gb, ge;
     bin_range(a, gb, ge);
     for (int g0 = gb; g0 < ge; g0 += kBinSub)
@@ -504,35 +543,46 @@ __global__ void __launch_bounds__(1024) tile_ranges_kernel(int T, uint32_t* __re
 
 hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st) {
     if (a.T <= 0) return hipSuccess;
+    // with the LDS binning the tile order comes with the scatter (bin_scatter_kernel's extra
+    // workgroup, or tile_order_kernel when nothing is scattered: launch_bin_order)
+    const bool lds = a.P > 0 && a.hist;
     if (a.P > 0) {
-        if (a.hist) {
+        if (lds) {
             const hipError_t e = allow_lds(bin_count_kernel, bin_lds_bytes(a.T));
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(bin_count_kernel, dim3(a.nblk), dim3(kBinThreads), bin_lds_bytes(a.T), st, a);
-            hipLaunchKernelGGL(bin_totals_kernel, dim3((a.T + 63) / 64), dim3(1024), 0, st, a);
+            hipLaunchKernelGGL(bin_colscan_kernel, dim3((a.T + 63) / 64), dim3(1024), 0, st, a);
         } else {
             hipLaunchKernelGGL(bin_atomic_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
         }
     }
+    uint32_t* ord = lds ? nullptr : order;
     if (a.T <= 8 * 1024)
-        hipLaunchKernelGGL(tile_ranges_kernel<8>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
+        hipLaunchKernelGGL(tile_ranges_kernel<8>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, ord);
     else if (a.T <= 40 * 1024)
-        hipLaunchKernelGGL(tile_ranges_kernel<40>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
+        hipLaunchKernelGGL(tile_ranges_kernel<40>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, ord);
     else
-        hipLaunchKernelGGL(tile_ranges_kernel<0>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, order);
-    if (a.P > 0 && a.hist) hipLaunchKernelGGL(bin_offsets_kernel, dim3((a.T + 63) / 64), dim3(1024), 0, st, a);
+        hipLaunchKernelGGL(tile_ranges_kernel<0>, dim3(1), dim3(1024), 0, st, a.T, a.tile_work, ranges, ord);
     return hipGetLastError();
 }
 
-hipError_t launch_bin_scatter(const BinArgs& a, hipStream_t st) {
+hipError_t launch_bin_scatter(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st) {
     if (a.P <= 0 || a.T <= 0) return hipSuccess;
     if (a.hist) {
         const hipError_t e = allow_lds(bin_scatter_kernel, bin_lds_bytes(a.T));
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(bin_scatter_kernel, dim3(a.nblk), dim3(kBinThreads), bin_lds_bytes(a.T), st, a);
+        hipLaunchKernelGGL(bin_scatter_kernel, dim3(a.nblk + 1), dim3(kBinThreads), bin_lds_bytes(a.T), st, a, ranges,
+                           order);
     } else {
         hipLaunchKernelGGL(bin_atomic_kernel<true>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
     }
+    return hipGetLastError();
+}
+
+// the tile order when the LDS binning ran but nothing was scattered (no instances)
+hipError_t launch_bin_order(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st) {
+    if (a.T <= 0 || !(a.P > 0 && a.hist)) return hipSuccess;
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, a.T, ranges, order);
     return hipGetLastError();
 }
 

@@ -55,7 +55,6 @@ struct BinArgs {
     const uint32_t* depth_keys;  // [P] float bits of each Gaussian's view depth
     uint2* pairs;             // [L] scatter pass: (depth bits, Gaussian) of each instance, grouped by tile
     uint32_t* flags;          // [L] scatter pass: backward row flags of each slot, zeroed
-    float4* records;          // scatter pass: each visible Gaussian's first slot (render record)
 };
 constexpr int kBinThreads = 1024;                  // binning workgroup (one per CU)
 constexpr int kBinSub = 1024;                      // Gaussians staged in LDS at a time
@@ -227,7 +226,8 @@ __global__ void preprocess_kernel(PreprocessArgs a);
 __global__ void mark_visible_kernel(int P, const float* means3D, const float* view, uint8_t* present);
 // counts, tile ranges, the longest-first tile order and every workgroup's scatter positions
 hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st);
-hipError_t launch_bin_scatter(const BinArgs& a, hipStream_t st);
+hipError_t launch_bin_scatter(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st);
+hipError_t launch_bin_order(const BinArgs& a, uint2* ranges, uint32_t* order, hipStream_t st);
 // sorts the tiles longer than min_n instances (the forward sorts the others when fused)
 hipError_t launch_tile_depth_sort(int T, const uint2* ranges, const uint32_t* order, const uint2* pairs,
                                   uint32_t* point_list, uint32_t* kA, uint32_t* vA, uint32_t* kB, int min_n,

@@ -249,11 +249,11 @@ struct ProfScope {
     }
 };
 
-// Pinned host word + event for the num_rendered readback, one per (host thread, device): a
+// Pinned host words for the num_rendered readback, one per (host thread, device): a
 // thread's calls on one device are issued in order, so the slot is free again by its next call.
 struct Readback {
-    uint32_t* host = nullptr;
-    hipEvent_t ev = nullptr;
+    uint32_t* host = nullptr;      // pinned, coherent host words (num_rendered, the error flag)
+    uint32_t* host_dev = nullptr;  // the same words as the device addresses them
     uint32_t* dev_flag = nullptr;  // preprocess error flag (prefiltered runs only)
 };
 static hipError_t readback_slot(Readback** out) {
@@ -266,15 +266,47 @@ static hipError_t readback_slot(Readback** out) {
     Readback& r = slots[dev];
     if (!r.host) {
         void* p = nullptr;
-        if ((e = hipHostMalloc(&p, 64, hipHostMallocDefault)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&r.ev, hipEventDisableTiming)) != hipSuccess) {
+        if ((e = hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess) return e;
+        void* d = nullptr;
+        if ((e = hipHostGetDevicePointer(&d, p, 0)) != hipSuccess) {
             (void)hipHostFree(p);
             return e;
         }
         r.host = static_cast<uint32_t*>(p);
+        r.host_dev = static_cast<uint32_t*>(d);
     }
     *out = &r;
     return hipSuccess;
+}
+
+// num_rendered (and the prefiltered error flag) straight into the pinned host words: one tiny
+// kernel instead of a D2H copy (a blit kernel plus the copy engine's hand-back: 4.5 us + a 5.6 us gap
+// before the next kernel at M1, round 6)
+__global__ void publish_count_kernel(const uint32_t* __restrict__ total, const uint32_t* __restrict__ flag,
+                                     uint32_t* host) {
+    if (threadIdx.x == 0) {
+        if (flag) host[1] = *flag;
+        __threadfence_system();  // the flag before the count the host polls for
+        host[0] = *total;
+        __threadfence_system();
+    }
+}
+
+// The host waits for publish_count_kernel's word itself instead of an event behind the kernel: an
+// event record between two kernels of the stream cost a 5.5 us dispatch gap at M1 (round 6). The
+// word starts at kUnpublished (num_rendered < 2^31 never is); the stream is queried every few
+// thousand spins so a failed launch or a fault surfaces as its error instead of a hang.
+constexpr uint32_t kUnpublished = 0xffffffffu;
+static hipError_t wait_published(const Readback* rb, hipStream_t st) {
+    volatile uint32_t* w = rb->host;
+    for (uint64_t spin = 1;; ++spin) {
+        if (w[0] != kUnpublished) return hipSuccess;
+        if ((spin & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) return w[0] != kUnpublished ? hipSuccess : hipErrorUnknown;  // drained, no word
+            if (q != hipErrorNotReady) return q;
+        }
+    }
 }
 
 // InitializeStencil (rasterizer_impl.cu:203-209)
@@ -704,7 +736,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     binning.P = P; binning.grid_x = gx; binning.grid_y = gy; binning.rec4 = record_f4(S); binning.T = T;
     binning.offsets = geom.point_offsets; binning.means2D = geom.means2D; binning.radii = radii;
     binning.depth_keys = geom.depth_keys;
-    binning.tile_work = img.tile_work; binning.records = geom.records;
+    binning.tile_work = img.tile_work;
     {
         const bool lds = bin_blocks_max(T) > 0 && !opt.test_bin_atomic;  // test_bin_atomic: the fallback (tests)
         int nb = bin_blocks_max(T);
@@ -747,13 +779,12 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         size_t tb = geom.scan_temp_bytes;
         R3DG_CHECK_HIP(rocprim::inclusive_scan(geom.scan_temp, tb, geom.tiles_touched, geom.point_offsets,
                                                (size_t)P, rocprim::plus<uint32_t>(), st));
-        // num_rendered (rasterizer_impl.cu:259-263 reads it with a blocking cudaMemcpy): one 4-byte
-        // copy into pinned host memory and a wait on an event behind that copy only
-        R3DG_CHECK_HIP(hipMemcpyAsync(rb->host, geom.point_offsets + P - 1, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                      st));
-        if (s->prefiltered)
-            R3DG_CHECK_HIP(hipMemcpyAsync(rb->host + 1, rb->dev_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        R3DG_CHECK_HIP(hipEventRecord(rb->ev, st));
+        // num_rendered (rasterizer_impl.cu:259-263 reads it with a blocking cudaMemcpy): written by one
+        // tiny kernel into pinned coherent host memory, which the host polls (wait_published)
+        reinterpret_cast<volatile uint32_t*>(rb->host)[0] = kUnpublished;
+        hipLaunchKernelGGL(publish_count_kernel, dim3(1), dim3(64), 0, st, geom.point_offsets + P - 1,
+                           s->prefiltered ? rb->dev_flag : nullptr, rb->host_dev);
+        R3DG_CHECK_HIP(hipGetLastError());
         // binning passes that need only the scan: per-tile counts, ranges, the tile order and the
         // scatter positions run on the device while the host waits for num_rendered and allocates
         {
@@ -761,9 +792,9 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
             R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, st));
             R3DG_CHECK_LAUNCH(s->debug, st);
         }
-        R3DG_CHECK_HIP(hipEventSynchronize(rb->ev));
-        const uint32_t Lh = *rb->host;
-        R3DG_REQUIRE(!s->prefiltered || rb->host[1] == 0,
+        R3DG_CHECK_HIP(wait_published(rb, st));
+        const uint32_t Lh = *reinterpret_cast<volatile uint32_t*>(rb->host);
+        R3DG_REQUIRE(!s->prefiltered || reinterpret_cast<volatile uint32_t*>(rb->host)[1] == 0,
                      "rasterize_gaussians: point is filtered although prefiltered is set (the reference traps, "
                      "auxiliary.h:156-160)");
         R3DG_REQUIRE(Lh < (1u << 31), "rasterize_gaussians: too many tile instances");
@@ -780,6 +811,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         return R3DG_ERR_ALLOC;
     }
     BinningState bin = binning_state_from(bin_base, (size_t)L);
+    if (L == 0) R3DG_CHECK_HIP(launch_bin_order(binning, img.ranges, img.tile_order, st));  // (no scatter)
     if (L > 0) {
         // every instance to its tile's next position (also records each Gaussian's first slot),
         // then every tile by (depth bits, Gaussian id): the
@@ -787,7 +819,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         ProfScope ps(R3DG_PROF_SORT, st, true, opt.prof_sort_markers);
         binning.pairs = bin.pairs;
         binning.flags = nullptr;  // the rows reduction zeroes its flags itself (backward)
-        R3DG_CHECK_HIP(launch_bin_scatter(binning, st));
+        R3DG_CHECK_HIP(launch_bin_scatter(binning, img.ranges, img.tile_order, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
         // the default-shader blend sorts the tiles of up to kFusedSortMax instances itself
         R3DG_CHECK_HIP(launch_tile_depth_sort(T, img.ranges, img.tile_order, bin.pairs, bin.point_list,

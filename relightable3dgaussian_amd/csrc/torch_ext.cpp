@@ -31,7 +31,10 @@ void check(int rc, const char* what) {
 // empty tensor (numel 0) means "absent", as the reference's data_ptr of an empty tensor
 const float* opt_ptr(const torch::Tensor& t) { return t.numel() == 0 ? nullptr : t.data_ptr<float>(); }
 
+// every entry point's inputs go to its first tensor's device, which must be a GPU: a host tensor
+// is refused here, before its pointer could reach a kernel (there is no CPU path)
 torch::Tensor dev_contig(const torch::Tensor& t, const torch::Device& dev) {
+    TORCH_CHECK(dev.is_cuda(), "the HIP rasterizer takes tensors on a GPU device, got ", dev);
     if (t.numel() == 0) return t;
     TORCH_CHECK(t.scalar_type() == torch::kFloat32, "expected a float32 tensor");
     return t.to(dev).contiguous();
