@@ -79,6 +79,8 @@ typedef struct r3dg_options {
     int test_bvh_lanes;       /* > 0: lanes per ray of the BVH opacity tracer (1, 2, 4, .. 64) */
     int test_bvh_sort;        /* 0 auto (Morton-sorted rays from 256k); 1 off; 2 on */
     int test_bvh_split;       /* 1: the static subtree-split tracer instead of the shared-stack groups */
+    int test_bin_one_pass;    /* 1: the one-pass binning scatter (per-(workgroup, tile) runs) instead of the
+                                 two passes through tile buckets (same results after the depth sort) */
 } r3dg_options;
 int r3dg_get_options(r3dg_options* out);   /* out->struct_size must be set */
 int r3dg_set_options(const r3dg_options* in);

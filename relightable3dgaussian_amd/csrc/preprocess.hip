@@ -410,21 +410,79 @@ __global__ void __launch_bounds__(kBinThreads) bin_scatter_kernel(BinArgs a, con
         return;
     }
     extern __shared__ uint32_t s_dyn[];
-    uint32_t* s_pos = s_dyn;  // [T] next position of this workgroup's instances of each tile
+    uint32_t* s_pos = s_dyn;  // [T] next position of this workgroup's instances of each tile (bucket)
     uint32_t* s_end = s_dyn + a.T;
     int* s_x0 = reinterpret_cast<int*>(s_end + kBinSub);
     int* s_y0 = s_x0 + kBinSub;
     int* s_w = s_y0 + kBinSub;
     const uint32_t* row = a.hist + (size_t)blockIdx.x * a.T;
-    // the workgroup's first position in each tile: the tile's first position + its column offset
-    for (int i = threadIdx.x; i < a.T; i += kBinThreads) s_pos[i] = a.tile_work[i] + row[i];
     int gb, ge;
     bin_range(a, gb, ge);
+    if (a.stage) {
+        // two-pass scatter, pass 1: the workgroup's first position in each bucket of kBinBucket tiles
+        // is the bucket's first position + its column offsets summed over the bucket's tiles, so a
+        // workgroup writes one run per bucket (~40 pairs at M1) instead of one per tile (~2.4)
+        const int nbk = (a.T + kBinBucket - 1) / kBinBucket;
+        for (int b = threadIdx.x; b < nbk; b += kBinThreads) {
+            const int t0 = b * kBinBucket, t1 = min(t0 + kBinBucket, a.T);
+            uint32_t s = a.tile_work[t0];
+            for (int t = t0; t < t1; ++t) s += row[t];
+            s_pos[b] = s;
+        }
+        for (int g0 = gb; g0 < ge; g0 += kBinSub)
+            bin_enumerate(a, g0, min(kBinSub, ge - g0), s_end, s_x0, s_y0, s_w, true,
+                          [&](uint32_t tile, uint32_t g, uint32_t key) {
+                              const uint32_t b = tile / kBinBucket;
+                              a.stage[atomicAdd(s_pos + b, 1u)] =
+                                  make_uint2(key, g | ((tile - b * kBinBucket) << kBinBucketShift));
+                          });
+        return;
+    }
+    // the workgroup's first position in each tile: the tile's first position + its column offset
+    for (int i = threadIdx.x; i < a.T; i += kBinThreads) s_pos[i] = a.tile_work[i] + row[i];
     for (int g0 = gb; g0 < ge; g0 += kBinSub)
         bin_enumerate(a, g0, min(kBinSub, ge - g0), s_end, s_x0, s_y0, s_w, true,
                       [&](uint32_t tile, uint32_t g, uint32_t key) {
                           a.pairs[atomicAdd(s_pos + tile, 1u)] = make_uint2(key, g);
                       });
+}
+
+// Two-pass scatter, pass 2: one workgroup per bucket moves the bucket's staged pairs (one contiguous
+// range of the list, in pass 1's order) to their tiles' ranges inside it, so every line of the
+// bucket's range is written through one L2 (pass 1's runs per (workgroup, tile) were ~2.4 pairs:
+// each line was written in pieces by ~7 workgroups on different XCDs). A wave ranks its 64 pairs
+// per tile by ballots; one lane per (wave, tile) claims the wave's positions from the tile's LDS
+// cursor. The order inside a tile is left unspecified, as the one-pass scatter's: the depth sort
+// (tile_depth_sort_kernel / the forward's fused sort) orders every tile by (depth bits, id).
+__global__ void __launch_bounds__(1024) bin_bucket_kernel(BinArgs a) {
+    __shared__ uint32_t s_cur[kBinBucket];
+    const int b = blockIdx.x;
+    const int t0 = b * kBinBucket, nt = min(kBinBucket, a.T - t0);
+    const int t = threadIdx.x, l = t & 63;
+    if (t < nt) s_cur[t] = a.tile_work[t0 + t];
+    const uint32_t s0 = a.tile_work[t0];
+    const uint32_t s1 = t0 + kBinBucket < a.T ? a.tile_work[t0 + kBinBucket] : a.L;
+    __syncthreads();
+    const uint32_t idmask = (1u << kBinBucketShift) - 1u;
+    for (uint32_t i0 = s0; i0 < s1; i0 += 1024) {
+        const uint32_t i = i0 + (uint32_t)t;
+        const bool valid = i < s1;
+        const uint2 kv = valid ? a.stage[i] : make_uint2(0u, 0u);
+        const int sub = valid ? (int)(kv.y >> kBinBucketShift) : -1;
+        // rank of the lane among the wave's pairs of its tile; lane s < kBinBucket counts tile s
+        uint32_t rank = 0, cnt = 0;
+#pragma unroll
+        for (int s = 0; s < kBinBucket; ++s) {
+            const unsigned long long m = __ballot(sub == s);
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (sub == s) rank = r;
+            if (l == s) cnt = (uint32_t)__builtin_popcountll(m);
+        }
+        // lanes 0..15 claim the wave's positions of their tile (one LDS atomic instruction)
+        const uint32_t base_l = cnt ? atomicAdd(&s_cur[l & (kBinBucket - 1)], cnt) : 0u;
+        const uint32_t base = (uint32_t)__shfl((int)base_l, sub & (kBinBucket - 1));
+        if (valid) a.pairs[base + rank] = make_uint2(kv.x, kv.y & idmask);
+    }
 }
 
 // Fallback above kBinMaxTiles tiles: one global atomic per instance on the per-tile counters
@@ -573,6 +631,8 @@ hipError_t launch_bin_scatter(const BinArgs& a, uint2* ranges, uint32_t* order, 
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(bin_scatter_kernel, dim3(a.nblk + 1), dim3(kBinThreads), bin_lds_bytes(a.T), st, a, ranges,
                            order);
+        if (a.stage)  // pass 2: the bucketed pairs to their tiles
+            hipLaunchKernelGGL(bin_bucket_kernel, dim3((a.T + kBinBucket - 1) / kBinBucket), dim3(1024), 0, st, a);
     } else {
         hipLaunchKernelGGL(bin_atomic_kernel<true>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
     }

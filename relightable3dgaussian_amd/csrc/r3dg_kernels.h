@@ -55,7 +55,13 @@ struct BinArgs {
     const uint32_t* depth_keys;  // [P] float bits of each Gaussian's view depth
     uint2* pairs;             // [L] scatter pass: (depth bits, Gaussian) of each instance, grouped by tile
     uint32_t* flags;          // [L] scatter pass: backward row flags of each slot, zeroed
+    uint2* stage;             // [L] two-pass scatter: the pairs grouped by tile bucket (Gaussian id | the
+                              // tile's index in its bucket << 28); null: one pass straight to the tiles
+    uint32_t L;               // scatter passes: instances in all
 };
+// Two-pass scatter: buckets of kBinBucket consecutive tiles (one contiguous range of the sorted list)
+constexpr int kBinBucket = 16;
+constexpr int kBinBucketShift = 28;  // the tile's index in its bucket above the Gaussian id (P < 2^28)
 constexpr int kBinThreads = 1024;                  // binning workgroup (one per CU)
 constexpr int kBinSub = 1024;                      // Gaussians staged in LDS at a time
 constexpr int kBinMaxTiles = (163840 - 16 * kBinSub) / 4;  // LDS counters per workgroup (160 KiB)

@@ -36,6 +36,9 @@ static r3dg_options initial_options() {
     o.struct_size = sizeof(r3dg_options);
     const char* e = getenv("R3DG_BWD_REDUCE");
     o.bwd_reduce = (e && e[0] == 'r') ? R3DG_REDUCE_ROWS : R3DG_REDUCE_ATOMIC;
+#ifdef R3DG_EXP_BIN_ONE_PASS  // experiment builds (A/B of the binning scatter in bench.py)
+    o.test_bin_one_pass = 1;
+#endif
     return o;
 }
 static std::mutex g_opt_mu;
@@ -160,8 +163,10 @@ static BinningState carve_binning(uintptr_t p, size_t L, uintptr_t* end) {
     BinningState b{};
     b.point_list = carve<uint32_t>(p, L);
     b.pairs = carve<uint2>(p, L);
-    b.sort_k1 = carve<uint32_t>(p, L);
-    b.sort_v1 = carve<uint32_t>(p, L);
+    // sort_k1 | sort_v1 as one block: the two-pass scatter stages its bucketed pairs there (uint2[L])
+    // before the long-tile depth sort uses them
+    b.sort_k1 = reinterpret_cast<uint32_t*>(carve<uint2>(p, L));
+    b.sort_v1 = b.sort_k1 + L;
     b.sort_k2 = carve<uint32_t>(p, L);
     b.flags = carve<uint32_t>(p, L);
     b.contrib = carve<uint8_t>(p, L);
@@ -819,6 +824,11 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         ProfScope ps(R3DG_PROF_SORT, st, true, opt.prof_sort_markers);
         binning.pairs = bin.pairs;
         binning.flags = nullptr;  // the rows reduction zeroes its flags itself (backward)
+        binning.L = (uint32_t)L;
+        // two-pass scatter through tile buckets (the staged ids carry the tile's index in its bucket
+        // in their top bits); test_bin_one_pass: straight to the tiles
+        binning.stage = (!opt.test_bin_one_pass && P < (1 << kBinBucketShift)) ? reinterpret_cast<uint2*>(bin.sort_k1)
+                                                                                : nullptr;
         R3DG_CHECK_HIP(launch_bin_scatter(binning, img.ranges, img.tile_order, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
         // the default-shader blend sorts the tiles of up to kFusedSortMax instances itself

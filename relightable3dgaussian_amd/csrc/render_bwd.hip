@@ -462,6 +462,8 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             const float4 rr = st[(2 + q) * NB + ju];
             v[4 * q] = rr.x; v[4 * q + 1] = rr.y; v[4 * q + 2] = rr.z; v[4 * q + 3] = rr.w;
         }
+        // (the last row stays a ds_read_b96 at S = 11: the forward's whole-float4 read, R3DG_ATTR_B128,
+        // measured +0.4 % here, profiles/r06/b128_prio_ab)
         const float alpha = fminf(0.99f, opacity * G);
         const bool ok = live && p < last && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
         okv = ok;

@@ -222,6 +222,11 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
             }
 #endif
             if (contrib && !stop) {
+#if R3DG_ATTR_B128
+                // the unused pad channel kept live: one ds_read_b128 (4 LDS-array cycles) for the
+                // last row instead of a ds_read_b96 (8)
+                if constexpr ((4 + SMAX) % 4 != 0) asm volatile("" ::"v"(v[NA4 * 4 - 1]));
+#endif
                 const float wgt = alpha * T;
                 C[0] = __builtin_fmaf(v[0], wgt, C[0]);
                 C[1] = __builtin_fmaf(v[1], wgt, C[1]);

@@ -889,7 +889,7 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor> trace_bvh
 #define R3DG_OPTION_FIELDS(X)                                                                         \
     X(bwd_reduce) X(prof_sort_markers) X(test_bwd_dpp) X(test_bwd_wterms) X(test_no_cull)              \
     X(test_bin_atomic) X(test_bin_blocks) X(test_tile_order_spatial) X(test_bwd_srs) X(test_bvh_lanes) \
-    X(test_bvh_sort) X(test_bvh_split)
+    X(test_bvh_sort) X(test_bvh_split) X(test_bin_one_pass)
 std::map<std::string, int64_t> get_options() {
     r3dg_options o{};
     o.struct_size = sizeof(o);

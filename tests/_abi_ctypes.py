@@ -47,7 +47,7 @@ class BackwardOutputs(C.Structure):  # r3dg_backward_outputs
 
 OPTION_FIELDS = ("bwd_reduce", "prof_sort_markers", "test_bwd_dpp", "test_bwd_wterms", "test_no_cull",
                  "test_bin_atomic", "test_bin_blocks", "test_tile_order_spatial", "test_bwd_srs", "test_bvh_lanes",
-                 "test_bvh_sort", "test_bvh_split")
+                 "test_bvh_sort", "test_bvh_split", "test_bin_one_pass")
 
 
 class Options(C.Structure):  # r3dg_options

@@ -553,6 +553,29 @@ def test_binning_atomic_path_matches(hip_ext):
     for k in ga:
         np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
 
+
+@rows_reduction()
+@pytest.mark.parametrize("size", [(480, 272), (1920, 1080)])
+def test_binning_one_pass_matches(hip_ext, size):
+    """The two-pass scatter through 16-tile buckets (default) and the one-pass scatter
+    (test_bin_one_pass) give bit-identical sorted lists, ranges, images and gradients; both match the
+    oracle's keys. 480x272: 510 tiles, a partial last bucket."""
+    cam = synthetic.m1_camera(*size)
+    scene = synthetic.m1_scene(P=60_000, S=11, seed=13, cam=cam)
+    a = hip_forward(hip_ext, scene, cam, S=11)
+    _keys_vs_oracle(hip_ext, scene, cam, a)
+    dc, do, dd, df = upstream_grads(cam.height, cam.width, 11, seed=3)
+    ga = hip_backward(hip_ext, a, dc, do, dd, df)
+    with lib_options(test_bin_one_pass=1):
+        b = hip_forward(hip_ext, scene, cam, S=11)
+        gb = hip_backward(hip_ext, b, dc, do, dd, df)
+    _keys_vs_oracle(hip_ext, scene, cam, b)
+    for k in ["color", "opacity", "depth", "feature", "n_contrib"]:
+        np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
+    for k in ga:
+        np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
+
+
 def test_brdf_complex_matches_oracle_and_golden(hip_ext):
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "brdf_pi5.npz"))
     inp = {k: g[k] for k in ["base", "rough", "metal", "normals", "viewdirs", "incidents", "visibility", "env"]}
