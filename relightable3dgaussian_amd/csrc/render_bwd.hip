@@ -339,6 +339,11 @@ __device__ __forceinline__ void split_bf16x2(const float (&x)[8], bf16x8& h, bf1
 #else
 #define R3DG_FLUSH_ADD(p, v) atomicAdd((p), (v))
 #endif
+#ifndef R3DG_BWD_ORIGIN_MOMENTS
+#define R3DG_BWD_ORIGIN_MOMENTS 1  // atomic flush: moments re-centred on the image origin in the D lanes
+                                   // (gather_bwd_kernel expands them about the mean); 0: expanded about
+                                   // the mean in the flush through LDS tiles (round 5)
+#endif
 #ifndef R3DG_BWDG_NB
 #define R3DG_BWDG_NB 64  // instances per staged batch of the DMA-staged kernel
 #endif
@@ -506,6 +511,13 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         }
     // pad lanes of the moment stores: the quadrant centre (row_sum expands the moments about the mean)
     const float cpad = nch == 6 ? qcx : qcy;
+    // atomic flush, origin moments: lane column c's re-centring constants (the moment about the image
+    // origin G_c = s_c + oka s0 + okb s1 + okc s2; products of half-integers < 2^14: exact in double)
+    const double dcx = (double)qcx, dcy = (double)qcy;
+    const double oka = nch == 1 ? dcx : nch == 2 ? dcy : nch == 3 ? dcx * dcx : nch == 4 ? dcx * dcy
+                     : nch == 5 ? dcy * dcy : 0.0;
+    const double okb = nch == 3 ? 2.0 * dcx : nch == 4 ? dcy : 0.0;
+    const double okc = nch == 4 ? dcx : nch == 5 ? 2.0 * dcy : 0.0;
     // atomic flush: this lane's column of the per-Gaussian sums, and the row stride in bytes
     float* const lane_sums = a.sums + nch;
     const uint32_t srs = (uint32_t)a.SRS;
@@ -594,7 +606,39 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         wave_lds_sync();
         return;
 #endif
-        if constexpr (ATOM) {
+        if constexpr (ATOM && R3DG_BWD_ORIGIN_MOMENTS) {
+            // The moments about the quadrant centre re-centred on the image origin in double, in the
+            // D registers' own lanes: lane c < 6 of each 16-lane row holds moment c of its rows
+            // 4g + i, and G_c = s_c + ka s0 + kb s1 + kc s2 (the wave's constants for column c,
+            // X = qcx + x, Y = qcy + y) takes s0, s1, s2 from lanes 0-2 of its row by DPP
+            // row_newbcast: no LDS round trip and no per-row mean. gather_bwd_kernel expands the
+            // summed origin moments about the Gaussian's mean in double (|X| <= ~8e3 px: the terms
+            // are <= ~6e7 times the moments they cancel to, far inside double's 2^-53).
+            double ev[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float sv = accY[i];
+                const float s0 = __builtin_amdgcn_mov_dpp(sv, 0x150, 0xf, 0xf, true);
+                const float s1 = __builtin_amdgcn_mov_dpp(sv, 0x151, 0xf, 0xf, true);
+                const float s2 = __builtin_amdgcn_mov_dpp(sv, 0x152, 0xf, 0xf, true);
+                ev[i] = __builtin_fma(okc, (double)s2, __builtin_fma(okb, (double)s1, __builtin_fma(oka, (double)s0, (double)sv)));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = (l >> 4) * 4 + i;
+                // (only the atomics under lane masks; adding 0 from the masked lanes instead
+                // measured 23x slower: rows past the group all name one Gaussian and contend)
+                const bool ok = row < r;
+                float* dst = lane_sums + (uint64_t)rid[i] * srs;
+#pragma unroll
+                for (int xb = 0; xb < NXB; ++xb)
+                    if (ok && xb * 16 + nch < 4 + S) R3DG_FLUSH_ADD(dst + xb * 16, accX[xb][i]);
+                double* mom = reinterpret_cast<double*>(a.sums + (uint64_t)rid[i] * srs + XW);
+                if (ok && nch < 6) R3DG_FLUSH_ADD(mom + nch, ev[i]);
+            }
+            wave_lds_sync();
+            return;
+        } else if constexpr (ATOM) {
             // The moments about the quadrant centre, expanded about the Gaussian's mean once per row
             // and summed in double: D rows go through a 16 x 8 float tile in w rows 0-1 (free once
             // the MFMA operands were read); lane rr = l & 15 expands row rr in double (expand_moments'
@@ -785,7 +829,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 wr[GRP * WQS] = qv0;
                 const uint32_t id0 = __builtin_amdgcn_readlane(row_l, j0);
                 if (lane0) {
-                    *reinterpret_cast<float2*>(wq + r * WQS + 64) = xy0;
+                    if constexpr (!R3DG_BWD_ORIGIN_MOMENTS) *reinterpret_cast<float2*>(wq + r * WQS + 64) = xy0;
                     reinterpret_cast<uint32_t*>(wq)[(GRP + r) * WQS + 64] = id0;
                 }
             }
@@ -795,7 +839,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
                 wr[GRP * WQS] = qv1;
                 const uint32_t id1 = __builtin_amdgcn_readlane(row_l, j1);
                 if (lane0) {
-                    *reinterpret_cast<float2*>(wq + (r + 1) * WQS + 64) = xy1;
+                    if constexpr (!R3DG_BWD_ORIGIN_MOMENTS) *reinterpret_cast<float2*>(wq + (r + 1) * WQS + 64) = xy1;
                     reinterpret_cast<uint32_t*>(wq)[(GRP + r + 1) * WQS + 64] = id1;
                 }
             }
@@ -1346,10 +1390,27 @@ __global__ void __launch_bounds__(256) gather_bwd_kernel(GatherBwdArgs a) {
             x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
         }
         if (a.sums_moments) {
-            // the atomic flush summed the moments about the mean in double (render_bwd_glds_kernel):
-            // dL/dmean2D, dL/dconic and dL/dopacity from them in double, rounded once
+            // the atomic flush summed the moments in double (render_bwd_glds_kernel): about the image
+            // origin (R3DG_BWD_ORIGIN_MOMENTS), expanded here about the mean (dx = mean - pixel), or
+            // about the mean already; dL/dmean2D, dL/dconic and dL/dopacity from them in double,
+            // rounded once
             const double2* md = reinterpret_cast<const double2*>(row + XW);
+#if R3DG_BWD_ORIGIN_MOMENTS
+            double2 m0 = md[0], m1 = md[1], m2 = md[2];  // [G0, GX], [GY, GXX], [GXY, GYY]
+            {
+                const float2 mu = a.means2D[g];
+                const double mx = mu.x, my = mu.y, G0 = m0.x, GX = m0.y, GY = m1.x;
+                const double sdx = mx * G0 - GX, sdy = my * G0 - GY;
+                const double sxx = mx * (sdx - GX) + m1.y;              // mx^2 G0 - 2 mx GX + GXX
+                const double sxy = mx * sdy - my * GX + m2.x;           // mx my G0 - mx GY - my GX + GXY
+                const double syy = my * (sdy - GY) + m2.y;              // my^2 G0 - 2 my GY + GYY
+                m0 = make_double2(G0, sdx);
+                m1 = make_double2(sdy, sxx);
+                m2 = make_double2(sxy, syy);
+            }
+#else
             const double2 m0 = md[0], m1 = md[1], m2 = md[2];
+#endif
             const float4 co = a.conic_opacity[g];
             const double o = -0.5 * (double)co.w;
             x[XW + 0] = (float)(o * a.W * ((double)co.x * m0.y + (double)co.y * m1.x));
