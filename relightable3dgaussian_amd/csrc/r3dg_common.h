@@ -74,7 +74,7 @@ struct BinningState {
     uint32_t* sort_v1;      // [L]
     uint32_t* sort_k2;      // [L]
     uint32_t* flags;        // [L] backward row flags, one byte per (slot, quadrant) (render_bwd.hip)
-    uint8_t* contrib;       // [L] per sorted position: bit q = a pixel of quadrant q blended it (forward)
+    uint8_t* contrib;       // [L] per sorted position: bit 2q + h = a pixel of half h of quadrant q blended it (forward)
 };
 struct ImageState {
     float* final_T;     // [H*W]
@@ -452,6 +452,36 @@ __device__ __forceinline__ bool quadrant_live(float2 xy, float4 staged, float qx
     const float det = co.x * co.z - co.y * co.y;
     if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return true;
     return !rect_culled(co, xy.x, xy.y, qx, qx + 7.0f, qy, qy + 7.0f);
+}
+
+// quadrant_live for the quadrant's two 8x4 halves (rows qy..qy+3, qy+4..qy+7): the threshold, the
+// conic's reciprocals and Mmax over the whole quadrant (an upper bound of each half's: still
+// conservative) are shared; the form's minimum is taken over each half's rectangle.
+// The rectangle's edges come in wave-uniform (SGPR: readfirstlane by the caller), so they cost
+// no VGPRs in the 64-VGPR forward.
+__device__ __forceinline__ float uniform_f(float x) {
+    return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(x)));
+}
+__device__ __forceinline__ void half_live(float2 xy, float4 staged, float xa, float xb, float ya, float ym0,
+                                          float ym1, float yb, int cull, bool& top, bool& bot) {
+    top = bot = true;
+    if (!cull) return;
+    const float4 co = unstage_conic(staged);
+    if (co.w < 1.0f / 255.0f) {
+        top = bot = false;
+        return;
+    }
+    const float det = co.x * co.z - co.y * co.y;
+    if (!(det > 0.0f) || !(co.x > 0.0f) || !(co.z > 0.0f)) return;
+    const float mx = xy.x, my = xy.y;
+    const float ia = __builtin_amdgcn_rcpf(co.x), ic = __builtin_amdgcn_rcpf(co.z);
+    const float dxa = mx - xa, dxb = mx - xb, dya = my - ya, dyb = my - yb;
+    const float ab = fabsf(co.y);
+    const float mmax = (co.x + ab) * fmaxf(dxa * dxa, dxb * dxb) + (co.z + ab) * fmaxf(dya * dya, dyb * dyb);
+    const float t = 2.0f * __logf(255.0f * co.w) * (1.0f + R3DG_CULL_MARGIN) + R3DG_CULL_MARGIN +
+                    R3DG_CULL_REL * mmax;
+    top = !(qform_min_rect(co.x, co.y, co.z, ia, ic, mx, my, xa, xb, ya, ym0) > t);
+    bot = !(qform_min_rect(co.x, co.y, co.z, ia, ic, mx, my, xa, xb, ym1, yb) > t);
 }
 
 }  // namespace r3dg

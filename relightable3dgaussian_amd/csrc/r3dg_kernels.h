@@ -102,7 +102,7 @@ struct RenderFwdArgs {
     // the zero_n4 after its outputs (the stores drain under the other workgroups' blends); null: none
     float4* zero_sums;
     uint32_t zero_n4, zero_chunk;
-    uint8_t* contrib;     // [L] per sorted position: bit q set when a pixel of quadrant q blended it
+    uint8_t* contrib;     // [L] per sorted position: bit 2q + h set when a pixel of half h (rows 0-3 / 4-7) of quadrant q blended it
     FeatureLayout flay;
     // fused depth sort (default-shader kernel): tiles of up to kFusedSortMax instances are sorted
     // from the binning's (depth bits, id) pairs in the blend's prologue and their sorted ids written

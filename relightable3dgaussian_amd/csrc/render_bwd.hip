@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(kBlock) render_bwd_dpp_kernel(RenderBwdArgs a)
             const int p = hi - 1 - j;  // position in the tile range (reference `contributor`)
             if (p >= wmax) continue;   // no pixel of this wave reaches this far back
             const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
-            if (!((m >> w) & 1u)) continue;
+            if (!((m >> (2 * w)) & 3u)) continue;  // either half of quadrant w (render_fwd.hip)
             bool contrib = inside && p < last;
             float G = 0.f, alpha = 0.f;
             float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -358,7 +358,7 @@ __device__ __forceinline__ void split_bf16x2(const float (&x)[8], bf16x8& h, bf1
 // (global_load_lds_dwordx4, no VGPRs) while the waves blend batch b, so the record round trip is
 // off the critical path and a batch costs one block barrier. A wave visits exactly the staged
 // instances that at least one of its pixels blended in the forward: the forward's contribution
-// bits (render_fwd.hip, one byte per sorted position, bit = quadrant), loaded one batch ahead --
+// bits (render_fwd.hip, one byte per sorted position, bits 2q, 2q + 1 = the halves of quadrant q), loaded one batch ahead --
 // no footprint cull here and no instance without a partial row. The instance's slot comes from
 // the lane that loaded its bits (record_slot), so nothing but the records goes through LDS.
 // Staging buffer layout: column q (float4 q of the record) of instance t at [q * NB + t].
@@ -772,7 +772,7 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
         // this wave's partial row of instance l (4 * slot + quadrant), flagged here, once per
         // visited instance (rather than by the flush's row stores)
         uint32_t row_l = 0u;
-        const bool mine = (cbits >> w) & 1u;
+        const bool mine = (cbits >> (2 * w)) & 3u;  // bit 2w + h: half h of quadrant w blended it
         mask_t bits = (mask_t)__ballot(mine);
         const int lo = hi - wmax;  // instances j < lo lie beyond every pixel of this wave
         if (lo >= NB) bits = 0u;

@@ -11,7 +11,7 @@
 //     reference's alpha test on every pixel of the quadrant (tests/test_gpu_parity.py checks cull
 //     on == cull off bit for bit, also on needle-shaped splats);
 //   * every wave records which staged instances at least one of its pixels blended: one byte
-//     per sorted position (bit = quadrant), the exact visit list of the backward (render_bwd.hip);
+//     per sorted position (bit 2q + h = half h of quadrant q), the exact visit list of the backward;
 //   * early exit per wave (ballot) and per block (__syncthreads_count), as the reference;
 //   * XCD-aware tile order (r3dg_kernels.h).
 // render_fwd_glds_kernel<SMAX, true> blends the splat-shader colour as well (non-default splat shaders).
@@ -37,6 +37,9 @@ R3DG_EXP_READER(r3dg_exp_counters_fwd)
 // own quadrant. Staging layout: column q (float4 q of the render record) of instance j at
 // [q * NB + j].
 // ---------------------------------------------------------------------------------------------
+#ifndef R3DG_FWD_HALF
+#define R3DG_FWD_HALF 0  // 1: each 8x4 half of a wave's quadrant walks its own cull list (measured 3.4 % slower: profiles/r06/fwd_half_ab)
+#endif
 #ifndef R3DG_FWDG_NB
 #define R3DG_FWDG_NB 64  // instances per staged batch (two resident: 12.3 KB, 64 VGPRs -> 8 waves/SIMD;
                          // 128: 24.6 KB -> 6 waves/SIMD, measured 0.480 vs 0.447 ms at M1)
@@ -64,10 +67,10 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     // | the tile's sorted Gaussian ids (fused sort)]; the fused sort's scratch aliases the staging
     constexpr int SORT4 = (int)((sizeof(TileSortLds<kFusedSortMax / kSortBT>) + 15) / 16);
     constexpr int STG = 2 * SBUF > SORT4 ? 2 * SBUF : SORT4;  // float4 of staging / sort scratch
-    __shared__ float4 s_lds[STG + 32 + kFusedSortMax / 4];
+    __shared__ float4 s_lds[STG + 64 + kFusedSortMax / 4];
     uint8_t* const s_cf = reinterpret_cast<uint8_t*>(s_lds + STG);
-    uint32_t* const s_ids = reinterpret_cast<uint32_t*>(s_lds + STG + 32);
-    if (threadIdx.x < 128) reinterpret_cast<uint32_t*>(s_cf)[threadIdx.x] = 0u;  // before the first barrier
+    uint32_t* const s_ids = reinterpret_cast<uint32_t*>(s_lds + STG + 64);
+    reinterpret_cast<uint32_t*>(s_cf)[threadIdx.x] = 0u;  // 2 x 64 x 8 flag bytes, before the first barrier
 
     const int tile = block_tile(a.tile_order, a.num_tiles);
     if (tile >= a.num_tiles) return;
@@ -155,18 +158,19 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // Contribution bits for the backward (render_bwd.hip): the byte of sorted position p holds bit
-    // q when a pixel of quadrant q blended instance p. Every accumulating lane of wave w sets the LDS
-    // flag byte [batch buffer][instance][w] (all write the same 1: no per-step ballot or scalar
-    // work); after the next batch barrier wave 0 folds each instance's four flag bytes into the
-    // contribution byte, stores it and clears the flags for their reuse two batches on.
-    // Positions past a block's early exit are never written: the backward only visits positions
-    // below the tile's largest n_contrib.
+    // 2q + h when a pixel of half h (rows 0-3 / 4-7) of quadrant q blended instance p. Every
+    // accumulating lane of wave w sets the LDS flag byte [batch buffer][instance][2w + h] (all write
+    // the same 1: no per-step ballot or scalar work); after the next batch barrier wave 0 folds each
+    // instance's eight flag bytes into the contribution byte, stores it and clears the flags for
+    // their reuse two batches on. Positions past a block's early exit are never written: the
+    // backward only visits positions below the tile's largest n_contrib.
     auto write_bits = [&](int b0, int cnt, int bb) {
         if (w == 0 && l < cnt) {
-            uint32_t* f = reinterpret_cast<uint32_t*>(s_cf) + 64 * bb + l;
-            const uint32_t fw = *f;
-            *f = 0u;
-            const uint32_t v = (fw & 1u) | (fw >> 7 & 2u) | (fw >> 14 & 4u) | (fw >> 21 & 8u);
+            uint2* f = reinterpret_cast<uint2*>(s_cf) + 64 * bb + l;
+            const uint2 fw = *f;
+            *f = make_uint2(0u, 0u);
+            const uint32_t v = (fw.x & 1u) | (fw.x >> 7 & 2u) | (fw.x >> 14 & 4u) | (fw.x >> 21 & 8u) |
+                               ((fw.y & 1u) | (fw.y >> 7 & 2u) | (fw.y >> 14 & 4u) | (fw.y >> 21 & 8u)) << 4;
             a.contrib[range.x + (uint32_t)(b0 + l)] = (uint8_t)v;
         }
     };
@@ -186,6 +190,20 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         }
         const float4* st = s_lds + buf * SBUF;
         const int cnt = min(NB, n - base);
+#if R3DG_FWD_HALF
+        // the exact cull per 8x4 half of the quadrant: one live mask per half
+        unsigned long long bt, bb;
+        {
+            bool mt = false, mb = false;
+            if (l < cnt) {
+                const float4 co = st[l], r1 = st[NB + l];
+                half_live(make_float2(r1.x, r1.y), co, uniform_f(qx0), uniform_f(qx0 + 7.0f), uniform_f(qy0),
+                          uniform_f(qy0 + 3.0f), uniform_f(qy0 + 4.0f), uniform_f(qy0 + 7.0f), a.cull, mt, mb);
+            }
+            bt = __ballot(mt);
+            bb = __ballot(mb);
+        }
+#else
         unsigned long long bits[NH];
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
@@ -197,9 +215,15 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
             }
             bits[h] = __ballot(mine);
         }
+#endif
+        // j: the staged instance (R3DG_FWD_HALF: per lane, one per half of the wave)
         auto step = [&](int j, bool live, float opacity, float power, float G) {
 #pragma clang fp contract(off)  // explicit FMAs only: both unrolled copies round alike
+#if R3DG_FWD_HALF
+            const int ju = j;
+#else
             const int ju = __builtin_amdgcn_readfirstlane(j);
+#endif
             float v[NA4 * 4];
 #pragma unroll
             for (int q = 0; q < NA4; ++q) {
@@ -243,9 +267,43 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 Op += wgt;
                 T = test_T;
                 last = (uint32_t)(base + j + 1);
-                s_cf[(buf * 64 + ju) * 4 + w] = 1;  // every accumulating lane writes the same byte
+                s_cf[(buf * 64 + ju) * 8 + 2 * w + (l >> 5)] = 1;  // every accumulating lane of a half: one byte
             }
         };
+#if R3DG_FWD_HALF
+        // Each half of the wave walks its own live list, two instances per iteration; a half whose
+        // 32 pixels are all done, or whose list ran out, idles (live = false) while the other walks on.
+        const bool top = l < 32;
+        {
+            const unsigned long long nd = __ballot(!done);
+            if ((uint32_t)nd == 0u) bt = 0ull;
+            if ((uint32_t)(nd >> 32) == 0u) bb = 0ull;
+        }
+        while (bt | bb) {
+            const int t0 = bt ? (int)__builtin_ctzll(bt) : -1;
+            bt &= bt - 1;
+            const int t1 = bt ? (int)__builtin_ctzll(bt) : -1;
+            bt &= bt - 1;
+            const int b0 = bb ? (int)__builtin_ctzll(bb) : -1;
+            bb &= bb - 1;
+            const int b1 = bb ? (int)__builtin_ctzll(bb) : -1;
+            bb &= bb - 1;
+            const int s0 = top ? t0 : b0, s1 = top ? t1 : b1;
+            const bool live0 = s0 >= 0, live1 = s1 >= 0;
+            const int j0 = live0 ? s0 : 0, j1 = live1 ? s1 : j0;  // valid staging slots either way
+            const float4 co0 = st[j0], co1 = st[j1];
+            const float2 xy0 = *reinterpret_cast<const float2*>(st + NB + j0);
+            const float2 xy1 = *reinterpret_cast<const float2*>(st + NB + j1);
+            const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
+            const float pw1 = gauss_power(co1, xy1.x - pfx, xy1.y - pfy);
+            const f32x2 G = {blend_expf(pw0), blend_expf(pw1)};
+            step(j0, live0, co0.w, pw0, G.x);
+            step(j1, live1, co1.w, pw1, G.y);
+            const unsigned long long nd = __ballot(!done);
+            if ((uint32_t)nd == 0u) bt = 0ull;
+            if ((uint32_t)(nd >> 32) == 0u) bb = 0ull;
+        }
+#else
         bool alive = __ballot(!done) != 0ull;
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
@@ -274,6 +332,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 if (__ballot(!done) == 0ull) alive = false;
             }
         }
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         buf ^= 1;
     }
