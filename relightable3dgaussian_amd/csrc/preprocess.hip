@@ -169,6 +169,9 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     // the per-tile counters of the atomic binning (bin_atomic_kernel) start at zero
     if (a.tile_count)
         for (int i = idx; i < a.num_tiles; i += (int)(gridDim.x * 256)) a.tile_count[i] = 0u;
+    // the single-pass scan's status words and ticket (rasterizer.hip scan_touched_kernel) start at zero
+    if (a.scan_status)
+        for (int i = idx; i < a.scan_words; i += (int)(gridDim.x * 256)) a.scan_status[i] = 0ull;
     if (use_sh) {
         const float* src = a.sh + (size_t)g0 * M3;
         // (a plain division here: the multiply-high of gather_bwd_kernel measured 2-5 % slower in
@@ -319,6 +322,9 @@ __global__ void __launch_bounds__(kBinThreads) bin_count_kernel(BinArgs a) {
     int* s_y0 = s_x0 + kBinSub;
     int* s_w = s_y0 + kBinSub;
     for (int i = threadIdx.x; i < a.T; i += kBinThreads) s_cnt[i] = 0u;
+    // bin_colscan_kernel's look-back status words and ticket start at zero
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < (a.T + 63) / 64 + 1; i += kBinThreads) a.tile_scan[i] = 0ull;
     int gb, ge;
     bin_range(a, gb, ge);
     for (int g0 = gb; g0 < ge; g0 += kBinSub)
@@ -335,20 +341,53 @@ __global__ void __launch_bounds__(kBinThreads) bin_count_kernel(BinArgs a) {
 // (one per lane), wave w of 16 owns the contiguous rows [w nblk / 16, (w + 1) nblk / 16). One launch
 // for what were two (the totals, then the offsets after the ranges: round 6, one kernel boundary
 // fewer on the binning's critical path); the scatter adds the tile's first position.
-__global__ void __launch_bounds__(1024) bin_colscan_kernel(BinArgs a) {
+//
+// Round 6: the tiles' ranges and first positions as well (what tile_ranges_kernel computed in a
+// launch of its own, one 1024-thread workgroup scanning all T counts: 11 us at M1), by a decoupled
+// look-back over the workgroups' 64-tile totals (status words a.tile_scan, zeroed by bin_count_kernel;
+// the workgroup's logical id from a ticket, as scan_touched_kernel's).
+constexpr uint64_t kTileScanAggregate = 1ull << 62, kTileScanInclusive = 2ull << 62;
+__global__ void __launch_bounds__(1024) bin_colscan_kernel(BinArgs a, uint2* __restrict__ ranges) {
     __shared__ uint32_t s_part[16][64];
+    __shared__ int s_blk;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int tile = blockIdx.x * 64 + l;
+    const int nbk = (a.T + 63) / 64;
+    if (threadIdx.x == 0)
+        s_blk = (int)__hip_atomic_fetch_add(a.tile_scan + nbk, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int blk = s_blk;
+    const int tile = blk * 64 + l;
     const int r0 = w * a.nblk / 16, r1 = (w + 1) * a.nblk / 16;
     uint32_t s = 0;
     if (tile < a.T)
         for (int b = r0; b < r1; ++b) s += a.hist[(size_t)b * a.T + tile];
     s_part[w][l] = s;
     __syncthreads();
-    if (tile >= a.T) return;
     uint32_t run = 0;
     for (int k = 0; k < w; ++k) run += s_part[k][l];
-    if (w == 15) a.tile_work[tile] = run + s;  // the column total
+    if (w == 15) {
+        // the column totals of this workgroup's 64 tiles -> their first positions
+        const uint32_t cnt = tile < a.T ? run + s : 0u;
+        uint32_t x = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (l >= o) x += y;
+        }
+        const uint32_t agg = __shfl(x, 63);
+        if (blk > 0 && l == 0)
+            __hip_atomic_store(a.tile_scan + blk, kTileScanAggregate | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t prefix = lookback_prefix(a.tile_scan, blk);
+        if (l == 0)
+            __hip_atomic_store(a.tile_scan + blk, kTileScanInclusive | (prefix + agg), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t start = prefix + x - cnt;
+        if (tile < a.T) {
+            a.tile_work[tile] = start;  // the tile's first position
+            ranges[tile] = cnt ? make_uint2(start, start + cnt) : make_uint2(0u, 0u);
+        }
+    }
+    if (tile >= a.T) return;
     for (int b = r0; b < r1; ++b) {
         uint32_t* h = a.hist + (size_t)b * a.T + tile;
         const uint32_t c = *h;
@@ -609,7 +648,9 @@ hipError_t launch_bin_prepare(const BinArgs& a, uint2* ranges, uint32_t* order, 
             const hipError_t e = allow_lds(bin_count_kernel, bin_lds_bytes(a.T));
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(bin_count_kernel, dim3(a.nblk), dim3(kBinThreads), bin_lds_bytes(a.T), st, a);
-            hipLaunchKernelGGL(bin_colscan_kernel, dim3((a.T + 63) / 64), dim3(1024), 0, st, a);
+            // column scan + the tiles' ranges and first positions (no tile_ranges_kernel)
+            hipLaunchKernelGGL(bin_colscan_kernel, dim3((a.T + 63) / 64), dim3(1024), 0, st, a, ranges);
+            return hipGetLastError();
         } else {
             hipLaunchKernelGGL(bin_atomic_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
         }

@@ -485,3 +485,35 @@ __device__ __forceinline__ void half_live(float2 xy, float4 staged, float xa, fl
 }
 
 }  // namespace r3dg
+
+namespace r3dg {
+// Decoupled look-back by one wave (single-pass scans, rasterizer.hip scan_touched_kernel /
+// preprocess.hip bin_colscan_kernel): the exclusive prefix of workgroup b from the 64-bit status
+// words of its predecessors ([flag: 62-63 | value: 0-31], flag 1 = the workgroup's aggregate, 2 = its
+// inclusive prefix, 0 = not published yet). Lane k polls predecessor b - 1 - k, so a window of 64
+// predecessors costs one round of device-scope loads (each one crosses the XCDs' L2s): the window
+// is summed up to its nearest inclusive prefix once every word up to it is published, else polled
+// again. Called by all 64 lanes of one wave; returns the prefix in every lane.
+__device__ __forceinline__ uint32_t lookback_prefix(const uint64_t* status, int b) {
+    const int l = threadIdx.x & 63;
+    uint32_t prefix = 0;
+    int hi = b;  // predecessors [0, hi) not summed yet
+    while (hi > 0) {
+        const int p = hi - 1 - l;
+        const uint64_t s = p >= 0 ? __hip_atomic_load(status + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+                                  : (2ull << 62);  // before workgroup 0: an inclusive prefix of 0
+        const uint32_t flag = (uint32_t)(s >> 62);
+        const unsigned long long incl = __ballot(flag == 2u), ready = __ballot(flag != 0u);
+        const int stop = incl ? (int)__builtin_ctzll(incl) : 63;  // the nearest inclusive prefix, or the window
+        const unsigned long long need = stop == 63 ? ~0ull : ((2ull << stop) - 1ull);
+        if ((ready & need) != need) continue;  // a word up to it is not published yet: poll again
+        uint32_t v = l <= stop ? (uint32_t)s : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+        prefix += v;
+        if (incl) break;
+        hi -= 64;
+    }
+    return prefix;
+}
+}  // namespace r3dg

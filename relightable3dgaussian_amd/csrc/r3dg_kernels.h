@@ -38,6 +38,8 @@ struct PreprocessArgs {
     unsigned int* error_flag;
     uint32_t* tile_count;  // [num_tiles] zeroed here for the atomic binning (bin_atomic_kernel), or null
     int num_tiles;
+    uint64_t* scan_status; // [scan_words] zeroed here for the single-pass scan (scan_touched_kernel), or null
+    int scan_words;
 };
 
 // Binning (duplicateWithKeys + SortPairs + identifyTileRanges, rasterizer_impl.cu:72-140, 343-383)
@@ -58,6 +60,7 @@ struct BinArgs {
     uint2* stage;             // [L] two-pass scatter: the pairs grouped by tile bucket (Gaussian id | the
                               // tile's index in its bucket << 28); null: one pass straight to the tiles
     uint32_t L;               // scatter passes: instances in all
+    uint64_t* tile_scan;      // [T / 64 + 1] bin_colscan_kernel's look-back status words and ticket
 };
 // Two-pass scatter: buckets of kBinBucket consecutive tiles (one contiguous range of the sorted list)
 constexpr int kBinBucket = 16;

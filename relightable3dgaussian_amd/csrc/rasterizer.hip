@@ -70,12 +70,9 @@ FeatureLayout make_feature_layout(int S, long long HW, bool native) {
 }
 
 // ---- state buffer layouts --------------------------------------------------------------------
-static size_t scan_temp_size(size_t P) {
-    size_t bytes = 0;
-    uint32_t* d = nullptr;
-    rocprim::inclusive_scan(nullptr, bytes, d, d, P, rocprim::plus<uint32_t>(), 0);
-    return bytes;
-}
+// the single-pass scan's status words (scan_touched_kernel): one per workgroup + the ticket counter
+int scan_blocks(size_t P);
+static size_t scan_temp_size(size_t P) { return sizeof(uint64_t) * ((size_t)scan_blocks(P) + 1); }
 
 // ---- the backward's atomic sums, prepared by the forward (RenderFwdArgs::zero_sums) -------------
 // Row stride (floats) of the per-Gaussian sums of the atomic flush: [X part (f32) | 6 moments (f64) |
@@ -181,7 +178,11 @@ size_t binning_state_bytes(size_t L) {
 BinningState binning_state_from(void* base, size_t L) { return carve_binning((uintptr_t)base, L, nullptr); }
 
 static int num_tiles_of(int H, int W) { return ((W + kTileX - 1) / kTileX) * ((H + kTileY - 1) / kTileY); }
-static size_t bin_hist_count(size_t T) { return (size_t)bin_blocks_max((int)T) * T; }
+// the binning's per-workgroup tile counts, then (8-B aligned) bin_colscan_kernel's look-back status
+// words and ticket
+static size_t bin_hist_words(size_t T) { return ((size_t)bin_blocks_max((int)T) * T + 1) & ~(size_t)1; }
+static size_t bin_hist_count(size_t T) { return bin_hist_words(T) + 2 * ((T + 63) / 64 + 1); }
+static uint64_t* bin_tile_scan(uint32_t* hist, size_t T) { return reinterpret_cast<uint64_t*>(hist + bin_hist_words(T)); }
 
 static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end, bool with_hist = true) {
     ImageState s{};
@@ -284,20 +285,94 @@ static hipError_t readback_slot(Readback** out) {
     return hipSuccess;
 }
 
-// num_rendered (and the prefiltered error flag) straight into the pinned host words: one tiny
-// kernel instead of a D2H copy (a blit kernel plus the copy engine's hand-back: 4.5 us + a 5.6 us gap
-// before the next kernel at M1, round 6)
-__global__ void publish_count_kernel(const uint32_t* __restrict__ total, const uint32_t* __restrict__ flag,
-                                     uint32_t* host) {
-    if (threadIdx.x == 0) {
-        if (flag) host[1] = *flag;
-        __threadfence_system();  // the flag before the count the host polls for
-        host[0] = *total;
-        __threadfence_system();
+// Inclusive scan of tiles_touched -> point_offsets (rasterizer_impl.cu:255-257 cub::InclusiveSum) in
+// one pass, and num_rendered published by the last workgroup: replaces rocPRIM's scan (an init
+// kernel + the scan kernel) and a one-thread publish kernel -- three launches, 18 us at M1 (round 6),
+// for 8 MB of traffic. The count goes straight into the pinned host words (a D2H copy cost a blit
+// kernel plus the copy engine's hand-back: 4.5 us + a 5.6 us gap before the next kernel). Workgroup b scans its kScanItems contiguous items in registers / LDS and
+// publishes its aggregate, then its inclusive prefix, in status[b] (decoupled look-back: flag in
+// the top bits of one 64-bit word with the value, so one atomic load reads both). status[] is zeroed
+// by preprocess_kernel, which runs before on the same stream. The grid (<= P / 16384 workgroups, 62
+// at M1) is co-resident, so the look-back spins only while a predecessor is still summing.
+constexpr int kScanThreads = 1024, kScanIPT = 16, kScanItems = kScanThreads * kScanIPT;
+constexpr uint64_t kScanAggregate = 1ull << 62, kScanInclusive = 2ull << 62;
+int scan_blocks(size_t P) { return (int)std::max<size_t>(1, (P + kScanItems - 1) / kScanItems); }
+__global__ void __launch_bounds__(kScanThreads) scan_touched_kernel(const uint32_t* __restrict__ in,
+                                                                    uint32_t* __restrict__ out, int P,
+                                                                    uint64_t* status,
+                                                                    const uint32_t* __restrict__ flag,
+                                                                    uint32_t* host) {
+    __shared__ uint32_t s_wave[kScanThreads / 64];
+    __shared__ uint32_t s_prefix;
+    __shared__ int s_b;
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    // the logical workgroup id from a ticket (status[gridDim.x], zeroed with the status words): a
+    // workgroup only ever waits for tickets drawn before its own, i.e. for running workgroups
+    if (t == 0) s_b = (int)__hip_atomic_fetch_add(status + gridDim.x, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int b = s_b;
+    const int i0 = b * kScanItems + t * kScanIPT;
+    uint32_t v[kScanIPT];
+    if (i0 + kScanIPT <= P) {
+        const uint4* src = reinterpret_cast<const uint4*>(in + i0);  // in: 256-B aligned, i0 % 16 == 0
+#pragma unroll
+        for (int k = 0; k < kScanIPT / 4; ++k) {
+            const uint4 q = src[k];
+            v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanIPT; ++k) v[k] = i0 + k < P ? in[i0 + k] : 0u;
+    }
+#pragma unroll
+    for (int k = 1; k < kScanIPT; ++k) v[k] += v[k - 1];
+    // exclusive scan of the thread totals across the workgroup
+    uint32_t x = v[kScanIPT - 1];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (l >= o) x += y;
+    }
+    if (l == 63) s_wave[w] = x;
+    __syncthreads();
+    uint32_t wpre = 0, agg = 0;
+#pragma unroll
+    for (int k = 0; k < kScanThreads / 64; ++k) {
+        const uint32_t s = s_wave[k];
+        wpre += k < w ? s : 0u;
+        agg += s;
+    }
+    const uint32_t texcl = wpre + x - v[kScanIPT - 1];
+    if (w == 0) {
+        if (b > 0 && l == 0)
+            __hip_atomic_store(status + b, kScanAggregate | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t prefix = lookback_prefix(status, b);
+        if (l == 0) {
+            __hip_atomic_store(status + b, kScanInclusive | (prefix + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            s_prefix = prefix;
+            if (b == (int)gridDim.x - 1) {  // the total: num_rendered into the pinned host words
+                if (flag) host[1] = *flag;
+                __threadfence_system();  // the flag before the count the host polls for
+                host[0] = prefix + agg;
+                __threadfence_system();
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t base = s_prefix + texcl;
+    if (i0 + kScanIPT <= P) {
+        uint4* dst = reinterpret_cast<uint4*>(out + i0);
+#pragma unroll
+        for (int k = 0; k < kScanIPT / 4; ++k)
+            dst[k] = make_uint4(base + v[4 * k], base + v[4 * k + 1], base + v[4 * k + 2], base + v[4 * k + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanIPT; ++k)
+            if (i0 + k < P) out[i0 + k] = base + v[k];
     }
 }
 
-// The host waits for publish_count_kernel's word itself instead of an event behind the kernel: an
+// The host waits for scan_touched_kernel's word itself instead of an event behind the kernel: an
 // event record between two kernels of the stream cost a 5.5 us dispatch gap at M1 (round 6). The
 // word starts at kUnpublished (num_rendered < 2^31 never is); the stream is queried every few
 // thousand spins so a failed launch or a fault surfaces as its error instead of a hang.
@@ -748,6 +823,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         if (opt.test_bin_blocks > 0) nb = std::min(nb, opt.test_bin_blocks);  // experiments
         binning.nblk = lds ? std::min(nb, (P + kBinSub - 1) / kBinSub) : 0;
         binning.hist = lds && P > 0 ? img.bin_hist : nullptr;
+        binning.tile_scan = binning.hist ? bin_tile_scan(img.bin_hist, (size_t)T) : nullptr;
     }
     if (P > 0) {
         PreprocessArgs pa{};
@@ -765,6 +841,8 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         pa.rgb = geom.rgb; pa.clamped = geom.clamped; pa.error_flag = nullptr;
         pa.tile_count = binning.hist ? nullptr : img.tile_work;  // the atomic binning's counters
         pa.num_tiles = T;
+        pa.scan_status = reinterpret_cast<uint64_t*>(geom.scan_temp);  // zeroed for scan_touched_kernel
+        pa.scan_words = scan_blocks((size_t)P) + 1;
         Readback* rb = nullptr;
         R3DG_CHECK_HIP(readback_slot(&rb));
         if (s->prefiltered) {
@@ -781,13 +859,12 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         }
         R3DG_CHECK_LAUNCH(s->debug, st);
 
-        size_t tb = geom.scan_temp_bytes;
-        R3DG_CHECK_HIP(rocprim::inclusive_scan(geom.scan_temp, tb, geom.tiles_touched, geom.point_offsets,
-                                               (size_t)P, rocprim::plus<uint32_t>(), st));
-        // num_rendered (rasterizer_impl.cu:259-263 reads it with a blocking cudaMemcpy): written by one
-        // tiny kernel into pinned coherent host memory, which the host polls (wait_published)
+        // offsets = inclusive scan of tiles_touched; num_rendered (rasterizer_impl.cu:259-263 reads it
+        // with a blocking cudaMemcpy) written by the scan's last workgroup into pinned coherent host
+        // memory, which the host polls (wait_published)
         reinterpret_cast<volatile uint32_t*>(rb->host)[0] = kUnpublished;
-        hipLaunchKernelGGL(publish_count_kernel, dim3(1), dim3(64), 0, st, geom.point_offsets + P - 1,
+        hipLaunchKernelGGL(scan_touched_kernel, dim3(scan_blocks((size_t)P)), dim3(kScanThreads), 0, st,
+                           geom.tiles_touched, geom.point_offsets, P, reinterpret_cast<uint64_t*>(geom.scan_temp),
                            s->prefiltered ? rb->dev_flag : nullptr, rb->host_dev);
         R3DG_CHECK_HIP(hipGetLastError());
         // binning passes that need only the scan: per-tile counts, ranges, the tile order and the
