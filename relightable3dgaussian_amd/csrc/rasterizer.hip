@@ -965,7 +965,13 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     ra.features = feats;
     ra.bg = s->bg;
     ra.S = S; ra.W = W; ra.H = H; ra.grid_x = gx; ra.num_tiles = T; ra.cull = 1;
-    ra.tile_order = nullptr;  // forward: XCD-aware spatial order (measured faster: L2 locality)
+#ifdef R3DG_EXP_FWD_SPATIAL  // experiment builds: the forward in the XCD-aware spatial order
+    ra.tile_order = nullptr;
+#else
+    // forward: longest tiles first, as the backward (round 6: render_fwd 0.507 -> 0.495 ms at M1,
+    // profiles/r06/fwd_order_ab; rounds 2-4 measured the spatial order faster, before the fused sort)
+    ra.tile_order = img.tile_order;
+#endif
     ra.final_T = img.final_T;
     ra.n_contrib = img.n_contrib;
     ra.out_color = out->color;
