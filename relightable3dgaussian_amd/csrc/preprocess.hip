@@ -172,6 +172,8 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     // the single-pass scan's status words and ticket (rasterizer.hip scan_touched_kernel) start at zero
     if (a.scan_status)
         for (int i = idx; i < a.scan_words; i += (int)(gridDim.x * 256)) a.scan_status[i] = 0ull;
+    if (a.work_hist)
+        for (int i = idx; i < kWorkBuckets; i += (int)(gridDim.x * 256)) a.work_hist[i] = 0u;
     if (use_sh) {
         const float* src = a.sh + (size_t)g0 * M3;
         // (a plain division here: the multiply-high of gather_bwd_kernel measured 2-5 % slower in

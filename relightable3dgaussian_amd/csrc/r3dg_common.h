@@ -82,6 +82,10 @@ struct ImageState {
     uint2* ranges;      // [tiles]
     uint32_t* tile_order;        // [padded tiles] tiles by descending instance count (blend launch order)
     uint32_t* tile_work;         // [tiles] binning: instance count per tile, then its first position
+    uint32_t* bwd_work;          // [tiles] the forward's count of the backward's work per tile
+    uint32_t* bwd_rank;          // [tiles] the tile's rank in its work bucket
+    uint32_t* bwd_hist;          // [1024] the work buckets' counts
+    uint32_t* bwd_order;         // [padded tiles] the backward's launch order (most work first)
     uint32_t* bin_hist;          // [bin_blocks_max(tiles), tiles] binning: per-workgroup counts / positions
 };
 

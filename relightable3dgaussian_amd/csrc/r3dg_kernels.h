@@ -40,6 +40,7 @@ struct PreprocessArgs {
     int num_tiles;
     uint64_t* scan_status; // [scan_words] zeroed here for the single-pass scan (scan_touched_kernel), or null
     int scan_words;
+    uint32_t* work_hist;   // [kWorkBuckets] zeroed here for the forward's work buckets (RenderFwdArgs::bwd_hist)
 };
 
 // Binning (duplicateWithKeys + SortPairs + identifyTileRanges, rasterizer_impl.cu:72-140, 343-383)
@@ -115,7 +116,15 @@ struct RenderFwdArgs {
     // non-default splat shaders: per Gaussian float4 [shader r, g, b, 0] (refresh_record_opacity
     // writes it after the splat shaders), staged as one more record column
     const float4* shader_rec;
+    // [T] the backward's work per tile (the most visits of any of its quadrants), or null; with it
+    // each tile's rank in its work bucket (bwd_rank [T]) from the bucket counts bwd_hist
+    // [kWorkBuckets] (zeroed by preprocess_kernel)
+    uint32_t* bwd_work;
+    uint32_t* bwd_rank;
+    uint32_t* bwd_hist;
 };
+constexpr int kWorkBuckets = 1024;
+__host__ __device__ inline int work_bucket(uint32_t work) { return (int)(work >> 2 < 1023u ? work >> 2 : 1023u); }
 constexpr int kFusedSortMax = 1024;
 
 // Per-Gaussian gradient sums the gather kernel assembles (LDS, one row per Gaussian):
@@ -212,6 +221,13 @@ struct XyzNormalArgs {
     const float* depth;
     float* normal;
     float* xyz;
+    // the backward's launch order, computed by the grid's extra column from the forward's per-tile
+    // work (RenderFwdArgs::bwd_work), or null
+    int num_tiles, blocks_x;   // blocks_x: pixel workgroups per row of the 1-D grid
+    const uint32_t* bwd_work;
+    const uint32_t* bwd_rank;
+    const uint32_t* bwd_hist;
+    uint32_t* bwd_order;
 };
 
 struct IntermediateArgs {
@@ -228,6 +244,7 @@ struct IntermediateArgs {
     const float4* records;  // render records (intermediate_glds_kernel stages conic + opacity, position)
     int rec4;
     float4* inter_rec;      // [P] scratch: [depth, stencil, stencil opacity, 0], packed per launch
+    const uint32_t* tile_order;  // launch order of the tiles (longest first), or null (XCD-aware spatial)
 };
 
 // kernels (defined in the .hip translation units)
@@ -262,8 +279,11 @@ __device__ __forceinline__ uint32_t instance_slot(const uint32_t* offsets, float
 #define R3DG_XYZ_R 4  // tile rows per xyz_normal_kernel workgroup (render_fwd.hip; 1 / 2 / 4 / 8: 25.7 / 25.0 / 21.7 / 24.9 us at M1)
 #endif
 __global__ void xyz_normal_kernel(XyzNormalArgs a);
+constexpr int kOrderSlices = 16;  // xyz_normal_kernel's leading workgroups that sort the backward's tile order
 // RenderIntermediateTextures: packs the per-Gaussian depth / stencil record, then the DMA-staged blend
 hipError_t launch_intermediate(const IntermediateArgs& a, int P, const int* radii, hipStream_t st);
+hipError_t launch_bwd_order(int T, const uint32_t* work, const uint32_t* rank, const uint32_t* hist, uint32_t* order,
+                            hipStream_t st);
 
 // host launchers for the templated blend kernels
 hipError_t launch_render_forward(const RenderFwdArgs& a, bool shader, hipStream_t stream);

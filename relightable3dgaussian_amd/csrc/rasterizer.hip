@@ -116,7 +116,12 @@ static float* take_prepared_sums(void* geom, int P, int S, int SRS) {
 // the backward's launch order: longest tiles first; test_tile_order_spatial the XCD-aware spatial
 // order (per-XCD-band orders measured and dropped)
 static const uint32_t* bwd_tile_order(const ImageState& is, const r3dg_options& opt) {
-    return opt.test_tile_order_spatial ? nullptr : is.tile_order;
+    if (opt.test_tile_order_spatial) return nullptr;
+#ifdef R3DG_EXP_BWD_COUNT_ORDER  // experiment builds: the binning's instance-count order
+    return is.tile_order;
+#else
+    return is.bwd_order;  // most backward work first (the forward's visit counts)
+#endif
 }
 
 // Carving works on an integer cursor so the same code computes sizes (base 0) and pointers.
@@ -193,6 +198,10 @@ static ImageState carve_image(uintptr_t p, int H, int W, uintptr_t* end, bool wi
     s.ranges = carve<uint2>(p, T);
     s.tile_order = carve<uint32_t>(p, padded_tile_grid((int)T));
     s.tile_work = carve<uint32_t>(p, T);
+    s.bwd_work = carve<uint32_t>(p, T);
+    s.bwd_rank = carve<uint32_t>(p, T);
+    s.bwd_hist = carve<uint32_t>(p, kWorkBuckets);
+    s.bwd_order = carve<uint32_t>(p, padded_tile_grid((int)T));
     // the binning's per-workgroup tile counts: last, so the backward's view of the buffer does
     // not depend on whether they live here (r3dg_rasterize_gaussians) or in transient scratch
     // (r3dg_rasterize_gaussians_ex)
@@ -843,6 +852,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         pa.num_tiles = T;
         pa.scan_status = reinterpret_cast<uint64_t*>(geom.scan_temp);  // zeroed for scan_touched_kernel
         pa.scan_words = scan_blocks((size_t)P) + 1;
+        pa.work_hist = img.bwd_hist;  // the forward's work buckets start at zero
         Readback* rb = nullptr;
         R3DG_CHECK_HIP(readback_slot(&rb));
         if (s->prefiltered) {
@@ -883,6 +893,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         L = (int)Lh;
     } else if (T > 0) {  // no Gaussians: every tile range empty
         R3DG_CHECK_HIP(hipMemsetAsync(img.tile_work, 0, sizeof(uint32_t) * (size_t)T, st));
+        R3DG_CHECK_HIP(hipMemsetAsync(img.bwd_hist, 0, sizeof(uint32_t) * kWorkBuckets, st));  // (no preprocess)
         R3DG_CHECK_HIP(launch_bin_prepare(binning, img.ranges, img.tile_order, st));
         R3DG_CHECK_LAUNCH(s->debug, st);
     }
@@ -922,6 +933,7 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     ia.stencil_opacity = geom.stencil_opacity; ia.W = W; ia.H = H; ia.grid_x = gx; ia.num_tiles = T;
     ia.out_depth = out->depth; ia.out_stencil = out->stencil;
     ia.records = geom.records; ia.rec4 = record_f4(S); ia.inter_rec = inter_rec;
+    ia.tile_order = img.tile_order;  // longest tiles first, as the blends
     if (splat_active) {
         // the splat shaders read the intermediate depth / stencil images
         R3DG_REQUIRE(out->depth && out->stencil, "rasterize_gaussians: splat shaders need depth and stencil outputs");
@@ -988,6 +1000,9 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
     ra.point_list_out = bin.point_list;
     ra.shader_rec = shader_rec;
     ra.cull = opt.test_no_cull ? 0 : 1;
+    ra.bwd_work = T > 0 ? img.bwd_work : nullptr;
+    ra.bwd_rank = img.bwd_rank;
+    ra.bwd_hist = img.bwd_hist;
     if (prepared_sums && T > 0) {
         ra.zero_sums = reinterpret_cast<float4*>(prepared_sums);
         ra.zero_n4 = (uint32_t)((size_t)sums_srs * (size_t)P / 4);
@@ -1004,9 +1019,15 @@ extern "C" int r3dg_rasterize_gaussians_ex(const r3dg_raster_settings* s, const 
         xa.W = W; xa.H = H; xa.view = s->viewmatrix; xa.focal_x = focal_x; xa.focal_y = focal_y;
         xa.cx = s->cx; xa.cy = s->cy; xa.opacity = out->opacity; xa.depth = out->depth;
         xa.normal = out->normal; xa.xyz = out->surface_xyz;
-        hipLaunchKernelGGL(xyz_normal_kernel, dim3(gx, (gy + R3DG_XYZ_R - 1) / R3DG_XYZ_R), dim3(256), 0, st, xa);
+        // kOrderSlices leading workgroups sort the backward's tile order (tile_order_by_work) meanwhile
+        xa.num_tiles = T; xa.bwd_work = img.bwd_work; xa.bwd_rank = img.bwd_rank; xa.bwd_hist = img.bwd_hist;
+        xa.bwd_order = T > 0 ? img.bwd_order : nullptr;
+        xa.blocks_x = gx;
+        hipLaunchKernelGGL(xyz_normal_kernel, dim3((T > 0 ? kOrderSlices : 0) + gx * ((gy + R3DG_XYZ_R - 1) / R3DG_XYZ_R)),
+                           dim3(256), 0, st, xa);
         R3DG_CHECK_LAUNCH(s->debug, st);
     } else {
+        if (T > 0) R3DG_CHECK_HIP(launch_bwd_order(T, img.bwd_work, img.bwd_rank, img.bwd_hist, img.bwd_order, st));
         if (out->normal) R3DG_CHECK_HIP(hipMemsetAsync(out->normal, 0, sizeof(float) * 3 * (size_t)H * W, st));
         if (out->surface_xyz)
             R3DG_CHECK_HIP(hipMemsetAsync(out->surface_xyz, 0, sizeof(float) * 3 * (size_t)H * W, st));

@@ -164,14 +164,26 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     // instance's eight flag bytes into the contribution byte, stores it and clears the flags for
     // their reuse two batches on. Positions past a block's early exit are never written: the
     // backward only visits positions below the tile's largest n_contrib.
+    // (wave 0 also counts the backward's visits per quadrant: the tile's backward work, below)
+    int vq0 = 0, vq1 = 0, vq2 = 0, vq3 = 0;
+    const bool wave0 = __builtin_amdgcn_readfirstlane(w) == 0;  // uniform: the counters stay scalar
     auto write_bits = [&](int b0, int cnt, int bb) {
-        if (w == 0 && l < cnt) {
-            uint2* f = reinterpret_cast<uint2*>(s_cf) + 64 * bb + l;
-            const uint2 fw = *f;
-            *f = make_uint2(0u, 0u);
-            const uint32_t v = (fw.x & 1u) | (fw.x >> 7 & 2u) | (fw.x >> 14 & 4u) | (fw.x >> 21 & 8u) |
-                               ((fw.y & 1u) | (fw.y >> 7 & 2u) | (fw.y >> 14 & 4u) | (fw.y >> 21 & 8u)) << 4;
-            a.contrib[range.x + (uint32_t)(b0 + l)] = (uint8_t)v;
+        if (wave0) {
+            uint32_t v = 0u;
+            if (l < cnt) {
+                uint2* f = reinterpret_cast<uint2*>(s_cf) + 64 * bb + l;
+                const uint2 fw = *f;
+                *f = make_uint2(0u, 0u);
+                v = (fw.x & 1u) | (fw.x >> 7 & 2u) | (fw.x >> 14 & 4u) | (fw.x >> 21 & 8u) |
+                    ((fw.y & 1u) | (fw.y >> 7 & 2u) | (fw.y >> 14 & 4u) | (fw.y >> 21 & 8u)) << 4;
+                a.contrib[range.x + (uint32_t)(b0 + l)] = (uint8_t)v;
+            }
+            if (a.bwd_work) {
+                vq0 += __builtin_popcountll(__ballot(v & 0x03u));
+                vq1 += __builtin_popcountll(__ballot(v & 0x0cu));
+                vq2 += __builtin_popcountll(__ballot(v & 0x30u));
+                vq3 += __builtin_popcountll(__ballot(v & 0xc0u));
+            }
         }
     };
     int buf = 0;
@@ -343,6 +355,15 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         write_bits(b0, n - b0, buf ^ 1);
     }
 
+    // the tile's backward work: the most visits any of its quadrants makes (the backward's batches are
+    // barrier-synchronised, so its slowest quadrant paces the workgroup); the backward's launch order
+    // sorts by it (xyz_normal_kernel's extra workgroup, tile_order_by_work)
+    if (a.bwd_work && wave0 && l == 0) {
+        const uint32_t work = (uint32_t)max(max(vq0, vq1), max(vq2, vq3));
+        a.bwd_work[tile] = work;
+        // the tile's rank in its work bucket (the order's bucket sort needs no atomics then)
+        a.bwd_rank[tile] = atomicAdd(a.bwd_hist + work_bucket(work), 1u);
+    }
     // the backward's atomic sums (RenderFwdArgs::zero_sums): this tile's share, after its blend
     if (!SHADER && a.zero_sums) {  // (training forwards only: never with splat shaders)
         const uint32_t z0 = (uint32_t)tile * a.zero_chunk, z1 = min(z0 + a.zero_chunk, a.zero_n4);
@@ -413,7 +434,7 @@ __global__ void __launch_bounds__(kBlock) intermediate_glds_kernel(IntermediateA
 #pragma clang fp contract(off)
     constexpr int NB = 64, NCOL = 3, SBUF = NCOL * NB;
     __shared__ float4 s_lds[2 * SBUF];
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int tile = block_tile(a.tile_order, a.num_tiles);
     if (tile >= a.num_tiles) return;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
@@ -541,12 +562,84 @@ __device__ __forceinline__ float3 surface_point(const XyzNormalArgs& a, int x, i
 #ifndef R3DG_XYZ_R
 #define R3DG_XYZ_R 4
 #endif
+// The backward's launch order from the forward's per-tile work counts (RenderFwdArgs::bwd_work): a
+// bucket sort by work / 4 (capped), descending, as the binning's instance-count order
+// (preprocess.hip tile_order_block). The forward counted the buckets and gave every tile its rank in
+// its bucket (global atomics, one per tile), so one 256-thread workgroup scans the 1024 bucket counts
+// and places every tile at its bucket's start + rank, with no atomics. The padded grid's last slots
+// name no tile (T).
+// Workgroup `slice` of `nslices` places tiles [T slice / nslices, T (slice + 1) / nslices) (every one
+// scans the bucket counts itself: 4 KB), so the placement's dependent loads spread over workgroups.
+__device__ void tile_order_by_work(int T, const uint32_t* __restrict__ work, const uint32_t* __restrict__ rank,
+                                   const uint32_t* __restrict__ hist, uint32_t* __restrict__ order, int slice,
+                                   int nslices, uint32_t* lds) {
+    constexpr int NT = 256, BPT = kWorkBuckets / NT;
+    uint32_t* const cur = lds;                   // [kWorkBuckets] (the caller's LDS)
+    uint32_t* const s_wave = lds + kWorkBuckets;  // [NT / 64]
+    const int t = threadIdx.x, l = t & 63, wv = t >> 6;
+    // exclusive scan in descending bucket order: thread t owns reversed buckets [BPT t, BPT t + BPT)
+    uint32_t c[BPT], sum = 0;
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+        c[k] = hist[kWorkBuckets - 1 - (BPT * t + k)];
+        sum += c[k];
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (l >= o) x += y;
+    }
+    if (l == 63) s_wave[wv] = x;
+    __syncthreads();
+    uint32_t run = x - sum;
+    for (int k = 0; k < wv; ++k) run += s_wave[k];
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+        cur[kWorkBuckets - 1 - (BPT * t + k)] = run;  // the bucket's first slot
+        run += c[k];
+    }
+    __syncthreads();
+    const int i0 = (int)((long long)T * slice / nslices), i1 = (int)((long long)T * (slice + 1) / nslices);
+    for (int i = i0 + t; i < i1; i += NT) order[cur[work_bucket(work[i])] + rank[i]] = (uint32_t)i;
+    if (slice == nslices - 1) {
+        const int TP = padded_tile_grid(T);
+        for (int i = T + t; i < TP; i += NT) order[i] = (uint32_t)T;
+    }
+}
+
+// the backward's tile order on its own (forwards that compute no pseudo normal)
+__global__ void __launch_bounds__(256) bwd_order_kernel(int T, const uint32_t* __restrict__ work,
+                                                        const uint32_t* __restrict__ rank,
+                                                        const uint32_t* __restrict__ hist, uint32_t* __restrict__ order) {
+    __shared__ uint32_t lds[kWorkBuckets + 4];
+    tile_order_by_work(T, work, rank, hist, order, blockIdx.x, gridDim.x, lds);
+}
+
+hipError_t launch_bwd_order(int T, const uint32_t* work, const uint32_t* rank, const uint32_t* hist, uint32_t* order,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(bwd_order_kernel, dim3((T + 1023) / 1024), dim3(256), 0, st, T, work, rank, hist, order);
+    return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) xyz_normal_kernel(XyzNormalArgs a) {
+    // the extra column of the grid: the backward's tile order, one slice of the tiles per workgroup
+    // (off the critical path)
+    // (a 1-D grid whose first kOrderSlices workgroups are dispatched first and finish long before
+    // the kernel's last pixel blocks; as a last grid column they lengthened it by ~4 us)
     // the block's 18 x (16 R + 2) neighbourhood (edge-clamped) of surface points, each evaluated
-    // once into LDS instead of nine times per pixel
+    // once into LDS instead of nine times per pixel (the order workgroups use the same array)
     constexpr int R = R3DG_XYZ_R, HW_ = 18, HH = 16 * R + 2;
+    static_assert(3 * HW_ * HH >= kWorkBuckets + 4, "the order's LDS fits the halo array");
     __shared__ float sp[3][HW_ * HH];
-    const int bx = blockIdx.x * 16, by = blockIdx.y * 16 * R;
+    const int nord = a.bwd_order ? kOrderSlices : 0;
+    if ((int)blockIdx.x < nord) {
+        tile_order_by_work(a.num_tiles, a.bwd_work, a.bwd_rank, a.bwd_hist, a.bwd_order, blockIdx.x, nord,
+                           reinterpret_cast<uint32_t*>(&sp[0][0]));
+        return;
+    }
+    const int pb = (int)blockIdx.x - nord, pbx = pb % a.blocks_x, pby = pb / a.blocks_x;
+    const int bx = pbx * 16, by = pby * 16 * R;
     for (int k = threadIdx.x; k < HW_ * HH; k += 256) {
         const int hx = min(max(bx + k % HW_ - 1, 0), a.W - 1), hy = min(max(by + k / HW_ - 1, 0), a.H - 1);
         const float3 q = surface_point(a, hx, hy);
