@@ -37,6 +37,9 @@ R3DG_EXP_READER(r3dg_exp_counters_fwd)
 // own quadrant. Staging layout: column q (float4 q of the render record) of instance j at
 // [q * NB + j].
 // ---------------------------------------------------------------------------------------------
+#ifndef R3DG_FWD_TSIGN
+#define R3DG_FWD_TSIGN 1  // the pixel's stop kept as T's sign (no done mask); 0: a done mask (rounds 1-5)
+#endif
 #ifndef R3DG_FWD_HALF
 #define R3DG_FWD_HALF 0  // 1: each 8x4 half of a wave's quadrant walks its own cull list (measured 3.4 % slower: profiles/r06/fwd_half_ab)
 #endif
@@ -112,8 +115,18 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         __syncthreads();
     }
 
+#if R3DG_FWD_TSIGN
+    // A pixel's stop is T's sign: the reference sets `done` when a contributing instance would take T
+    // below 1e-4 and keeps T; here T becomes -|T| (one v_cndmask with source modifiers), every later
+    // test_T = T (1 - alpha) < 0 stops again and leaves it there, and final_T is |T|. No separate
+    // done mask, which the compiler moved between SGPR and VGPR form at every step.
+    float T = inside ? 1.0f : -1.0f;
+#define R3DG_DONE (T < 0.0f)
+#else
     bool done = !inside;
     float T = 1.0f;
+#define R3DG_DONE done
+#endif
     uint32_t last = 0;
     float C[3] = {0.f, 0.f, 0.f}, F[SMAX > 0 ? SMAX : 1];
     float CS[SHADER ? 3 : 1];
@@ -191,7 +204,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
     for (; base < n; base += NB) {
         // batch `base` has landed (every wave waited for its own DMA) and nobody reads the other
         // buffer any more
-        const bool all_done = __syncthreads_count(done) == kBlock;
+        const bool all_done = __syncthreads_count(R3DG_DONE) == kBlock;
         // the previous batch's flags, before the DMA issue: folding them after wave 0's DMA issue
         // measured 0.556 vs 0.480 ms
         if (base > 0) write_bits(base - NB, NB, buf ^ 1);
@@ -244,10 +257,17 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 v[4 * q] = r.x; v[4 * q + 1] = r.y; v[4 * q + 2] = r.z; v[4 * q + 3] = r.w;
             }
             const float alpha = fminf(0.99f, opacity * G);  // bit-identical to the oracle
+#if R3DG_FWD_TSIGN
+            const bool contrib = live && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const float test_T = T * (1.0f - alpha);
+            const bool stop = test_T < 0.0001f;  // also every step after the pixel's stop (T < 0)
+            if (contrib && stop) T = -fabsf(T);
+#else
             const bool contrib = live && !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
             const float test_T = T * (1.0f - alpha);
             const bool stop = test_T < 0.0001f;
             done = done || (contrib && stop);
+#endif
 #ifdef R3DG_EXP_COUNT
             {
                 const unsigned long long acc_b = __ballot(contrib && !stop);
@@ -287,7 +307,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         // 32 pixels are all done, or whose list ran out, idles (live = false) while the other walks on.
         const bool top = l < 32;
         {
-            const unsigned long long nd = __ballot(!done);
+            const unsigned long long nd = __ballot(!R3DG_DONE);
             if ((uint32_t)nd == 0u) bt = 0ull;
             if ((uint32_t)(nd >> 32) == 0u) bb = 0ull;
         }
@@ -311,12 +331,12 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
             const f32x2 G = {blend_expf(pw0), blend_expf(pw1)};
             step(j0, live0, co0.w, pw0, G.x);
             step(j1, live1, co1.w, pw1, G.y);
-            const unsigned long long nd = __ballot(!done);
+            const unsigned long long nd = __ballot(!R3DG_DONE);
             if ((uint32_t)nd == 0u) bt = 0ull;
             if ((uint32_t)(nd >> 32) == 0u) bb = 0ull;
         }
 #else
-        bool alive = __ballot(!done) != 0ull;
+        bool alive = __ballot(!R3DG_DONE) != 0ull;
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
             unsigned long long b = bits[h];
@@ -341,7 +361,7 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
                 // converged here: a uniform exit (testing every 2 or 4 iterations instead, which
                 // drops ~10 scalar instructions per iteration, measured no faster)
-                if (__ballot(!done) == 0ull) alive = false;
+                if (__ballot(!R3DG_DONE) == 0ull) alive = false;
             }
         }
 #endif
@@ -369,6 +389,10 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
         const uint32_t z0 = (uint32_t)tile * a.zero_chunk, z1 = min(z0 + a.zero_chunk, a.zero_n4);
         for (uint32_t i = z0 + (uint32_t)t; i < z1; i += kBlock) a.zero_sums[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+#undef R3DG_DONE
+#if R3DG_FWD_TSIGN
+    T = fabsf(T);
+#endif
     if (inside) {
         const int pix = py * a.W + px;
         a.final_T[pix] = T;
