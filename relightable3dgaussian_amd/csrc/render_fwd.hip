@@ -40,6 +40,9 @@ R3DG_EXP_READER(r3dg_exp_counters_fwd)
 #ifndef R3DG_FWD_TSIGN
 #define R3DG_FWD_TSIGN 1  // the pixel's stop kept as T's sign (no done mask); 0: a done mask (rounds 1-5)
 #endif
+#ifndef R3DG_FWD_SWALK
+#define R3DG_FWD_SWALK 1  // the pair loop's live-mask walk by s_ff1 + s_bitset0 (inline asm)
+#endif
 #ifndef R3DG_FWD_HALF
 #define R3DG_FWD_HALF 0  // 1: each 8x4 half of a wave's quadrant walks its own cull list (measured 3.4 % slower: profiles/r06/fwd_half_ab)
 #endif
@@ -336,17 +339,29 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
             if ((uint32_t)(nd >> 32) == 0u) bb = 0ull;
         }
 #else
-        bool alive = __ballot(!R3DG_DONE) != 0ull;
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-            unsigned long long b = bits[h];
-            if (l == 0) R3DG_EXP_ADD(3, __builtin_popcountll(b));
-            while (alive && b) {
+        static_assert(NH == 1, "one 64-bit live mask per batch");
+        unsigned long long b = bits[0];
+        if (l == 0) R3DG_EXP_ADD(3, __builtin_popcountll(b));
+        if (__ballot(!R3DG_DONE) == 0ull) b = 0ull;  // (every pixel of the wave stopped)
+        {
+            constexpr int h = 0;
+            while (b) {
+#if R3DG_FWD_SWALK
+                // the pair from the live mask by s_ff1 + s_bitset0 (s_ff1 of an empty mask is -1, whose
+                // s_bitset0 clears the already clear bit 63): 4 scalar ops for what b &= b - 1 twice,
+                // two s_ff1 and their selects took 11
+                int j0, j1;
+                asm("s_ff1_i32_b64 %0, %2\n\ts_bitset0_b64 %2, %0\n\ts_ff1_i32_b64 %1, %2\n\ts_bitset0_b64 %2, %1"
+                    : "=&s"(j0), "=&s"(j1), "+s"(b));
+                const bool has1 = j1 >= 0;
+                j1 = has1 ? j1 : j0;
+#else
                 const int j0 = h * 64 + (int)__builtin_ctzll(b);
                 b &= b - 1;
                 const bool has1 = b != 0ull;
                 const int j1 = has1 ? h * 64 + (int)__builtin_ctzll(b) : j0;
                 b &= b - 1;
+#endif
                 const int u0 = __builtin_amdgcn_readfirstlane(j0), u1 = __builtin_amdgcn_readfirstlane(j1);
                 const float4 co0 = st[u0], co1 = st[u1];
                 const float2 xy0 = *reinterpret_cast<const float2*>(st + NB + u0);
@@ -360,8 +375,8 @@ render_fwd_glds_kernel(RenderFwdArgs a) {
                 step(j1, has1, co1.w, pw1, G.y);
                 if (l == 0) R3DG_EXP_ADD(2, has1 ? 2 : 1);
                 // converged here: a uniform exit (testing every 2 or 4 iterations instead, which
-                // drops ~10 scalar instructions per iteration, measured no faster)
-                if (__ballot(!R3DG_DONE) == 0ull) alive = false;
+                // drops ~10 scalar instructions per iteration, measured no faster in round 3)
+                if (__ballot(!R3DG_DONE) == 0ull) break;
             }
         }
 #endif
