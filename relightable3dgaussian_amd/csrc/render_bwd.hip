@@ -339,6 +339,9 @@ __device__ __forceinline__ void split_bf16x2(const float (&x)[8], bf16x8& h, bf1
 #else
 #define R3DG_FLUSH_ADD(p, v) atomicAdd((p), (v))
 #endif
+#ifndef R3DG_BWD_SWALK
+#define R3DG_BWD_SWALK 1  // the pair loop's live-mask walk by s_ff1 + s_bitset0 (inline asm), as the forward's
+#endif
 #ifndef R3DG_BWD_ORIGIN_MOMENTS
 #define R3DG_BWD_ORIGIN_MOMENTS 1  // atomic flush: moments re-centred on the image origin in the D lanes
                                    // (gather_bwd_kernel expands them about the mean); 0: expanded about
@@ -794,11 +797,28 @@ render_bwd_glds_kernel(RenderBwdArgs a) {
             return *reinterpret_cast<const float2*>(st + NB + __builtin_amdgcn_readfirstlane(j));
         };
         while (bits) {
+#if R3DG_BWD_SWALK
+            int j0, j1;
+            if constexpr (NB > 32) {
+                unsigned long long b = bits;
+                asm("s_ff1_i32_b64 %0, %2\n\ts_bitset0_b64 %2, %0\n\ts_ff1_i32_b64 %1, %2\n\ts_bitset0_b64 %2, %1"
+                    : "=&s"(j0), "=&s"(j1), "+s"(b));
+                bits = b;
+            } else {
+                uint32_t b = bits;
+                asm("s_ff1_i32_b32 %0, %2\n\ts_bitset0_b32 %2, %0\n\ts_ff1_i32_b32 %1, %2\n\ts_bitset0_b32 %2, %1"
+                    : "=&s"(j0), "=&s"(j1), "+s"(b));
+                bits = b;
+            }
+            const bool has1 = j1 >= 0;
+            j1 = has1 ? j1 : j0;
+#else
             const int j0 = (int)__builtin_ctzll(bits);
             bits &= bits - 1;
             const bool has1 = bits != 0u;
             const int j1 = has1 ? (int)__builtin_ctzll(bits) : j0;
             bits &= bits - 1;
+#endif
             const float4 co0 = rec0(j0), co1 = rec0(j1);
             const float2 xy0 = pos(j0), xy1 = pos(j1);
             const float pw0 = gauss_power(co0, xy0.x - pfx, xy0.y - pfy);
