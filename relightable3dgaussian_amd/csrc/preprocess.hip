@@ -360,9 +360,17 @@ __global__ void __launch_bounds__(1024) bin_colscan_kernel(BinArgs a, uint2* __r
     const int blk = s_blk;
     const int tile = blk * 64 + l;
     const int r0 = w * a.nblk / 16, r1 = (w + 1) * a.nblk / 16;
+    // the wave's rows of the column held in registers: all loads in flight at once, and the offsets
+    // pass below writes from them (a loop of dependent loads, twice: 20.2 -> 15.5 us at M1,
+    // profiles/r06/colscan_regs/)
+    constexpr int kRows = (R3DG_BIN_BLOCKS_MAX + 15) / 16;  // r1 - r0 <= ceil(nblk / 16)
+    uint32_t c[kRows];
     uint32_t s = 0;
-    if (tile < a.T)
-        for (int b = r0; b < r1; ++b) s += a.hist[(size_t)b * a.T + tile];
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+        c[k] = (tile < a.T && r0 + k < r1) ? a.hist[(size_t)(r0 + k) * a.T + tile] : 0u;
+        s += c[k];
+    }
     s_part[w][l] = s;
     __syncthreads();
     uint32_t run = 0;
@@ -390,11 +398,10 @@ __global__ void __launch_bounds__(1024) bin_colscan_kernel(BinArgs a, uint2* __r
         }
     }
     if (tile >= a.T) return;
-    for (int b = r0; b < r1; ++b) {
-        uint32_t* h = a.hist + (size_t)b * a.T + tile;
-        const uint32_t c = *h;
-        *h = run;
-        run += c;
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+        if (r0 + k < r1) a.hist[(size_t)(r0 + k) * a.T + tile] = run;
+        run += c[k];
     }
 }
 
