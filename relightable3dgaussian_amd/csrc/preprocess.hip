@@ -266,11 +266,10 @@ __device__ __forceinline__ void bin_enumerate(const BinArgs& a, int g0, int n, u
         const int g = g0 + i;
         s_end[i] = a.offsets[g] - base;
         const int r = a.radii[g];
+        const float2 m = a.means2D[g];  // loaded with the radius, not behind it: one round trip
+        asm volatile("" ::"v"(m.x), "v"(m.y));  // (kept here: the compiler sinks it into the branch)
         int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-        if (r > 0) {
-            const float2 m = a.means2D[g];
-            get_rect(m.x, m.y, r, a.grid_x, a.grid_y, x0, y0, x1, y1);
-        }
+        if (r > 0) get_rect(m.x, m.y, r, a.grid_x, a.grid_y, x0, y0, x1, y1);
         s_x0[i] = x0;
         s_y0[i] = y0;
         s_w[i] = max(x1 - x0, 1);
@@ -474,7 +473,12 @@ __global__ void __launch_bounds__(kBinThreads) bin_scatter_kernel(BinArgs a, con
         for (int b = threadIdx.x; b < nbk; b += kBinThreads) {
             const int t0 = b * kBinBucket, t1 = min(t0 + kBinBucket, a.T);
             uint32_t s = a.tile_work[t0];
-            for (int t = t0; t < t1; ++t) s += row[t];
+            if (t1 - t0 == kBinBucket) {  // all 16 loads in flight at once (a dependent loop: 8 round trips)
+#pragma unroll
+                for (int k = 0; k < kBinBucket; ++k) s += row[t0 + k];
+            } else {
+                for (int t = t0; t < t1; ++t) s += row[t];
+            }
             s_pos[b] = s;
         }
         for (int g0 = gb; g0 < ge; g0 += kBinSub)
