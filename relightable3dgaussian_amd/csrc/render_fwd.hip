@@ -590,9 +590,8 @@ hipError_t launch_intermediate(const IntermediateArgs& a, int P, const int* radi
 // forward.cu:564-658 (renderSurfaceXYZCUDA + renderPseudoNormalCUDA) fused: every thread
 // recomputes its 3x3 neighbourhood's surface points from depth/opacity (same expression as
 // the xyz it stores), so one pass produces both outputs.
-__device__ __forceinline__ float3 surface_point(const XyzNormalArgs& a, int x, int y) {
-    const int pix = y * a.W + x;
-    const float d = a.depth[pix] / fmaxf(a.opacity[pix], 0.0000001f);
+__device__ __forceinline__ float3 surface_point(const XyzNormalArgs& a, int x, int y, float depth, float opacity) {
+    const float d = depth / fmaxf(opacity, 0.0000001f);
     return make_float3(((float)x - a.cx) / a.focal_x * d, ((float)y - a.cy) / a.focal_y * d, d);
 }
 
@@ -679,15 +678,37 @@ __global__ void __launch_bounds__(256) xyz_normal_kernel(XyzNormalArgs a) {
     }
     const int pb = (int)blockIdx.x - nord, pbx = pb % a.blocks_x, pby = pb / a.blocks_x;
     const int bx = pbx * 16, by = pby * 16 * R;
-    for (int k = threadIdx.x; k < HW_ * HH; k += 256) {
-        const int hx = min(max(bx + k % HW_ - 1, 0), a.W - 1), hy = min(max(by + k / HW_ - 1, 0), a.H - 1);
-        const float3 q = surface_point(a, hx, hy);
-        sp[0][k] = q.x;
-        sp[1][k] = q.y;
-        sp[2][k] = q.z;
+    // every halo point's depth and opacity loaded first (all in flight at once), then evaluated
+    constexpr int NIT = (HW_ * HH + 255) / 256;
+    float dv[NIT], ov[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int k = (int)threadIdx.x + it * 256;
+        dv[it] = 0.f;
+        ov[it] = 0.f;
+        if (k < HW_ * HH) {
+            const int hx = min(max(bx + k % HW_ - 1, 0), a.W - 1), hy = min(max(by + k / HW_ - 1, 0), a.H - 1);
+            dv[it] = a.depth[hy * a.W + hx];
+            ov[it] = a.opacity[hy * a.W + hx];
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int k = (int)threadIdx.x + it * 256;
+        if (k < HW_ * HH) {
+            const int hx = min(max(bx + k % HW_ - 1, 0), a.W - 1), hy = min(max(by + k / HW_ - 1, 0), a.H - 1);
+            const float3 q = surface_point(a, hx, hy, dv[it], ov[it]);
+            sp[0][k] = q.x;
+            sp[1][k] = q.y;
+            sp[2][k] = q.z;
+        }
     }
     __syncthreads();
-    const float* v = a.view;
+    // the view rotation in registers, once: the xyz / normal stores may alias a.view, so the compiler
+    // re-read it per row, each read waited for
+    float v[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) v[i] = a.view[i];
 #pragma unroll
     for (int rr = 0; rr < R; ++rr) {
         const int lx = threadIdx.x & 15, ly = (threadIdx.x >> 4) + 16 * rr;
